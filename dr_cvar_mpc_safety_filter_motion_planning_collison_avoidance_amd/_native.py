@@ -1,0 +1,117 @@
+"""Loader for the HIP engine (``_lib/libdrcvar_halfspace.so``) — the C ABI of
+``include/drcvar_halfspace.h`` bound with ctypes.
+
+There is deliberately no fallback: if the shared library is missing or cannot be loaded every
+entry point raises :class:`NativeLibraryError`.  ``build()`` compiles it for gfx950 in-tree.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_DIR = os.path.join(PKG_DIR, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libdrcvar_halfspace.so")
+SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip")]
+INCLUDE_DIR = os.path.join(REPO_DIR, "include")
+HEADER = os.path.join(INCLUDE_DIR, "drcvar_halfspace.h")
+OFFLOAD_ARCH = os.environ.get("DRCVAR_OFFLOAD_ARCH", "gfx950")
+
+ABI_VERSION = 1
+OUT_WIDTH = 8
+MAX_SAMPLES = 16384
+COL_MEAN_H0, COL_MEAN_H1, COL_G_MEAN, COL_H0, COL_H1, COL_G_CVAR, COL_G_DR_STAR, COL_G_DR_TILDE = range(8)
+
+# return codes (include/drcvar_halfspace.h)
+OK, ERR_INVALID_ARGUMENT, ERR_UNSUPPORTED, ERR_LAUNCH = 0, 1, 2, 3
+
+# Every symbol include/drcvar_halfspace.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "drcvar_abi_version",
+    "drcvar_strerror",
+    "drcvar_safe_halfspaces_f64",
+    "drcvar_offsets_given_h_f64",
+    "drcvar_launch_plan",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP engine is not built or cannot be loaded (there is no CPU fallback)."""
+
+
+class EngineError(RuntimeError):
+    """A DRCVAR_* error code returned by the engine."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"drcvar error {code}: {message}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def build(verbose: bool = False, extra_flags=()) -> str:
+    """Compile the engine for gfx950 with hipcc into ``_lib/`` (works without a GPU)."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cmd = ["hipcc", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-I", INCLUDE_DIR, *extra_flags, *SOURCES, "-o", LIB_PATH + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def _bind(lib):
+    i64, dbl, ptr, i32p = ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)
+    lib.drcvar_abi_version.argtypes = []
+    lib.drcvar_abi_version.restype = ctypes.c_int
+    lib.drcvar_strerror.argtypes = [ctypes.c_int]
+    lib.drcvar_strerror.restype = ctypes.c_char_p
+    lib.drcvar_safe_halfspaces_f64.argtypes = [
+        ptr, i64, i64, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr]
+    lib.drcvar_safe_halfspaces_f64.restype = ctypes.c_int
+    lib.drcvar_offsets_given_h_f64.argtypes = [
+        ptr, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr]
+    lib.drcvar_offsets_given_h_f64.restype = ctypes.c_int
+    lib.drcvar_launch_plan.argtypes = [i64, i32p, i32p, i32p]
+    lib.drcvar_launch_plan.restype = ctypes.c_int
+    return lib
+
+
+def lib():
+    """The loaded engine library (raises NativeLibraryError if unavailable)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeLibraryError(
+                    f"HIP engine not built: {LIB_PATH} is missing (run __graft_entry__.build() or "
+                    f"python -m dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.build)")
+            try:
+                handle = ctypes.CDLL(LIB_PATH)
+            except OSError as exc:  # pragma: no cover - depends on the ROCm install
+                raise NativeLibraryError(f"cannot load {LIB_PATH}: {exc}") from exc
+            _bind(handle)
+            if handle.drcvar_abi_version() != ABI_VERSION:
+                raise NativeLibraryError("engine ABI version mismatch; rebuild the library")
+            _lib = handle
+    return _lib
+
+
+def check(code: int) -> None:
+    if code != OK:
+        raise EngineError(code, lib().drcvar_strerror(code).decode())
+
+
+def launch_plan(n_samples: int):
+    """(threads_per_unit, samples_per_thread, bins) chosen for ``n_samples`` (host-only query)."""
+    b, p, nb = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    check(lib().drcvar_launch_plan(int(n_samples), ctypes.byref(b), ctypes.byref(p), ctypes.byref(nb)))
+    return b.value, p.value, nb.value

@@ -1,0 +1,109 @@
+"""``simulation/environment.py`` — the caller that feeds the hot path, batched.
+
+Reference ``SafetyFilteringEnvironment.compute_safe_halfspaces_for_trajectory``
+(``simulation/environment.py:60-106``) loops over the horizon and, per step, over the obstacles,
+solving two LPs per (obstacle, step).  Here the whole horizon of every obstacle is ONE kernel
+launch: the per-obstacle ``[N, S+1, 2]`` sample trajectories are staged to the device once and
+handed to the kernel with their native strides (sample stride ``(S+1)*2``, step stride 2), so no
+transpose is made; obstacles with different N are grouped, one launch per distinct N.
+The return value keeps the reference's ``{'mean','cvar','dr_cvar'}`` -> ``[T][O]`` layout.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .. import engine
+from ..core import risk_metrics
+from ..core.halfspaces import HalfspaceBatch
+from ..engine import RiskParams
+
+
+def create_double_integrator_matrices(dt, dim=2):
+    """``core/dynamics.py:7-33`` (only ``C`` touches the hot path: environment.py:92)."""
+    A = np.block([[np.eye(dim), dt * np.eye(dim)], [np.zeros((dim, dim)), np.eye(dim)]])
+    B = np.block([[0.5 * dt ** 2 * np.eye(dim)], [dt * np.eye(dim)]])
+    C = np.block([np.eye(dim), np.zeros((dim, dim))])
+    return A, B, C
+
+
+class SafetyFilteringEnvironment:
+    def __init__(self, ROBOT_RADIUS, OBSTACLE_RADIUS, HORIZON, DT, ALPHA, DELTA, EPSILON):
+        self.ROBOT_RADIUS = ROBOT_RADIUS
+        self.OBSTACLE_RADIUS = OBSTACLE_RADIUS
+        self.HORIZON = HORIZON
+        self.DT = DT
+        self.ALPHA = ALPHA
+        self.DELTA = DELTA
+        self.EPSILON = EPSILON
+        self.A, self.B, self.C = create_double_integrator_matrices(DT)
+        self.n_states = self.A.shape[0]
+        self.n_inputs = self.B.shape[1]
+        self.n_outputs = self.C.shape[0]
+        self.state_bounds = None
+        self.input_bounds = None
+
+    @property
+    def params(self) -> RiskParams:
+        return RiskParams(self.ROBOT_RADIUS, self.OBSTACLE_RADIUS, self.ALPHA, self.DELTA,
+                          self.EPSILON)
+
+    def set_bounds(self, state_bounds=None, input_bounds=None):
+        self.state_bounds = state_bounds
+        self.input_bounds = input_bounds
+
+    def compute_halfspace_batch(self, obstacle_sample_trajectories, ego_ref_trajectory):
+        """Device-side result: a HalfspaceBatch whose record is [O, T, 8] (T = min(len(ref), H))."""
+        n_obstacles = len(obstacle_sample_trajectories)
+        n_steps = min(len(ego_ref_trajectory), self.HORIZON)               # environment.py:72
+        params = self.params
+        params.validate()
+        t0 = time.time()
+        dev = risk_metrics.device()
+        ego = np.asarray(ego_ref_trajectory, dtype=np.float64)[:n_steps] @ self.C.T  # :92
+        ego_d = torch.as_tensor(np.ascontiguousarray(ego)).to(dev)
+        record = torch.empty((n_obstacles, n_steps, engine.OUT_WIDTH), dtype=torch.float64,
+                             device=dev)
+        if n_obstacles == 0 or n_steps == 0:
+            return HalfspaceBatch(record)
+        groups: dict[int, list[int]] = {}
+        for i, tr in enumerate(obstacle_sample_trajectories):
+            groups.setdefault(int(np.shape(tr)[0]), []).append(i)
+        launches = []
+        for n, idx in groups.items():
+            # [G, N, n_steps, 2] slice of the reference layout, staged as-is (environment.py:88)
+            host = np.stack([np.asarray(obstacle_sample_trajectories[i], dtype=np.float64)[:, :n_steps, :]
+                             for i in idx])
+            dev_s = torch.as_tensor(host).to(dev)
+            view = dev_s.permute(0, 2, 1, 3)                                  # [G, T, N, 2] strided
+            launches.append((idx, view))
+        t1 = time.time()
+        for idx, view in launches:
+            out = engine.safe_halfspaces(view, ego_d, params)
+            if len(idx) == n_obstacles:
+                record = out
+            else:
+                record[torch.as_tensor(idx, device=dev)] = out
+        return HalfspaceBatch(record, setup_time=t1 - t0)
+
+    def compute_safe_halfspaces_for_trajectory(self, obstacle_sample_trajectories,
+                                               ego_ref_trajectory):
+        """Reference layout: ``{'mean','cvar','dr_cvar'}`` -> ``[T][O]`` SafeHalfspace lists."""
+        batch = self.compute_halfspace_batch(obstacle_sample_trajectories, ego_ref_trajectory)
+        t1 = time.time()
+        torch.cuda.synchronize()
+        batch.solve_time = time.time() - t1
+        return batch.to_lists()
+
+    def compute_distance_to_collision(self, ego_trajectory, obstacle_trajectories):
+        """Per-step minimum clearance (environment.py:108-140)."""
+        n_steps = min(len(ego_trajectory), len(obstacle_trajectories[0]))
+        distances = np.inf * np.ones(n_steps)
+        for t in range(n_steps):
+            ego_pos_t = self.C @ ego_trajectory[t]
+            for obs in obstacle_trajectories:
+                dist = np.linalg.norm(ego_pos_t - obs[t]) - self.ROBOT_RADIUS - self.OBSTACLE_RADIUS
+                distances[t] = min(distances[t], dist)
+        return distances

@@ -1,0 +1,32 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+GOLDEN_DIR = os.path.join(REPO, "tests", "golden")
+
+# Parity tolerance stated by the north star: offsets within 1e-6 absolute of the reference.
+OFFSET_TOL = 1e-6
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+def golden_files():
+    return sorted(glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+def load_golden(path):
+    z = np.load(path, allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(params=golden_files(), ids=lambda p: os.path.basename(p)[:-4])
+def golden(request):
+    return load_golden(request.param)

@@ -1,0 +1,93 @@
+"""CPU: the C-ABI library builds for gfx950, loads, exports exactly what include/*.h declares, and
+validates arguments on the host (no call here reaches the GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
+
+HEADER = os.path.join(REPO, "include", "drcvar_halfspace.h")
+
+
+def _declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(drcvar_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_bound_symbols():
+    assert _declared_functions() == sorted(_native.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.lib()
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (drcvar_\w+)", out))
+    assert exported == set(_declared_functions())
+
+
+def test_library_holds_gfx950_code_object():
+    blob = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version_and_strerror():
+    lib = _native.lib()
+    assert lib.drcvar_abi_version() == _native.ABI_VERSION == 1
+    assert lib.drcvar_strerror(0) == b"ok"
+    assert lib.drcvar_strerror(1) == b"invalid argument"
+    assert lib.drcvar_strerror(99) == b"unknown error"
+
+
+@pytest.mark.parametrize("n,expect", [(1, (64, 2, 128)), (100, (64, 2, 128)), (129, (128, 4, 256)),
+                                      (1000, (256, 4, 512)), (5000, (512, 16, 4096)),
+                                      (10000, (1024, 10, 4096)), (16384, (1024, 16, 4096))])
+def test_launch_plan(n, expect):
+    b, p, nb = _native.launch_plan(n)
+    assert (b, p, nb) == expect
+    assert b * p >= n and b % 64 == 0
+
+
+def test_launch_plan_rejects():
+    with pytest.raises(_native.EngineError) as e:
+        _native.launch_plan(0)
+    assert e.value.code == _native.ERR_INVALID_ARGUMENT
+    with pytest.raises(_native.EngineError) as e:
+        _native.launch_plan(_native.MAX_SAMPLES + 1)
+    assert e.value.code == _native.ERR_UNSUPPORTED
+
+
+def _call(lib, **kw):
+    a = dict(samples=16, O=1, T=1, N=10, so=20, st=20, sn=2, ego=16, es=2, rr=0.3, ro=0.3,
+             alpha=0.2, delta=0.1, eps=0.15, out=16)
+    a.update(kw)
+    return lib.drcvar_safe_halfspaces_f64(
+        ctypes.c_void_p(a["samples"]), a["O"], a["T"], a["N"], a["so"], a["st"], a["sn"],
+        ctypes.c_void_p(a["ego"]), a["es"], a["rr"], a["ro"], a["alpha"], a["delta"], a["eps"],
+        ctypes.c_void_p(a["out"]), None)
+
+
+def test_host_side_argument_validation():
+    lib = _native.lib()
+    assert _call(lib, N=0) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, alpha=0.0) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, alpha=-0.2) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, delta=float("nan")) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, O=-1) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, samples=0) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, out=0) == _native.ERR_INVALID_ARGUMENT
+    assert _call(lib, N=_native.MAX_SAMPLES + 1) == _native.ERR_UNSUPPORTED
+    # empty batches are a no-op (nothing is launched)
+    assert _call(lib, O=0) == _native.OK
+    assert _call(lib, T=0, samples=0, ego=0, out=0) == _native.OK
+    assert lib.drcvar_offsets_given_h_f64(None, 0, 5, 10, 2, None, 2, 0.3, 0.3, 0.2, 0.1, 0.15,
+                                          None, None) == _native.OK
+    assert lib.drcvar_offsets_given_h_f64(None, 3, 0, 10, 2, None, 2, 0.3, 0.3, 0.2, 0.1, 0.15,
+                                          None, None) == _native.ERR_INVALID_ARGUMENT

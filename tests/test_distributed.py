@@ -1,0 +1,70 @@
+"""CPU, world_size 2 over gloo: the multi-GPU partition + all-gather path
+(sharding.sharded_safe_halfspaces) reassembles exactly the single-process result.  The per-shard
+compute is the C oracle here (test-only injection); on the GPU box it is the HIP engine."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import sharding
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.engine import RiskParams
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_compute(samples_u, ego_u, p):
+    from oracle import c_oracle
+    u = samples_u.shape[0]
+    out = c_oracle.safe_halfspaces(samples_u.numpy()[None], ego_u.numpy(), p.robot_radius,
+                                   p.obstacle_radius, p.alpha, p.delta, p.epsilon)
+    return torch.from_numpy(out.reshape(u, 8))
+
+
+def _worker(rank, world, port, O, T, N, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(42)
+        samples = torch.from_numpy(rng.normal(size=(O, T, N, 2)))
+        ego = torch.from_numpy(rng.normal(size=(T, 2)))
+        full = sharding.sharded_safe_halfspaces(samples, ego, RiskParams(), compute=_oracle_compute)
+        local, a, b = sharding.sharded_safe_halfspaces(samples, ego, RiskParams(), gather=False,
+                                                       compute=_oracle_compute)
+        q.put((rank, full.numpy(), a, b, local.shape[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("O,T,N", [(3, 5, 40), (1, 3, 17), (10, 20, 100)])
+def test_two_rank_gather_matches_single_process(O, T, N):
+    from oracle import c_oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, O, T, N, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(42)
+    samples = rng.normal(size=(O, T, N, 2))
+    ego = rng.normal(size=(T, 2))
+    ref = c_oracle.safe_halfspaces(samples, ego, 0.3, 0.3, 0.2, 0.1, 0.15)
+    spans = {}
+    for rank, full, a, b, n_local in results:
+        np.testing.assert_array_equal(full, ref)
+        spans[rank] = (a, b)
+        assert b - a == n_local
+    assert spans[0][0] == 0 and spans[0][1] == spans[1][0] and spans[1][1] == O * T
