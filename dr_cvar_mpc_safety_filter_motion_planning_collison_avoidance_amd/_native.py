@@ -15,6 +15,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libdrcvar_halfspace.so")
+# diagnostic builds only (scripts/diag_stages.sh); the product always loads LIB_PATH
+LIB_PATH = os.environ.get("DRCVAR_DIAG_LIB", LIB_PATH)
 SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip")]
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 HEADER = os.path.join(INCLUDE_DIR, "drcvar_halfspace.h")
@@ -33,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "drcvar_abi_version",
     "drcvar_strerror",
     "drcvar_safe_halfspaces_f64",
+    "drcvar_safe_halfspaces_f64_ex",
     "drcvar_offsets_given_h_f64",
     "drcvar_launch_plan",
 )
@@ -75,6 +78,10 @@ def _bind(lib):
     lib.drcvar_safe_halfspaces_f64.argtypes = [
         ptr, i64, i64, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr]
     lib.drcvar_safe_halfspaces_f64.restype = ctypes.c_int
+    lib.drcvar_safe_halfspaces_f64_ex.argtypes = [
+        ptr, i64, i64, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr,
+        ctypes.c_int32, ctypes.c_int32]
+    lib.drcvar_safe_halfspaces_f64_ex.restype = ctypes.c_int
     lib.drcvar_offsets_given_h_f64.argtypes = [
         ptr, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr]
     lib.drcvar_offsets_given_h_f64.restype = ctypes.c_int

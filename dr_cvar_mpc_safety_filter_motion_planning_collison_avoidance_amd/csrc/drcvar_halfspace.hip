@@ -2,26 +2,31 @@
 //
 // One workgroup evaluates one unit = one (obstacle, horizon step): N fp64 samples xi_i in R^2.
 // Everything the reference does per unit in core/halfspaces.py:70-194 and core/risk_metrics.py:
-// 84-338 happens in ONE pass over HBM (16 B per sample, read once, coalesced 16-B/lane loads):
+// 84-338 happens in ONE pass over HBM (16 B per sample, read once, 16-B/lane coalesced loads):
 //
-//   1. load the samples into registers (P per thread), block-reduce their sum   -> mean mu
+//   1. load the samples into registers (P per thread); one block reduction gives the sums for the
+//      mean AND the (pivot-shifted) second moments                        [barrier 1]
 //   2. h = (mu - ego)/|mu - ego| ([1,0] if < 1e-10)            core/geometry.py:35-53
 //      mean halfspace from the origin                           core/halfspaces.py:84-94
-//   3. d_i = h . xi_i, block min/max                            core/risk_metrics.py:145,233
-//   4. exact (m+1)-th order statistic tau of d, m = floor(alpha*N), sort-free:
-//        value-linear histogram of d in LDS (NB bins, LDS atomics) -> scan -> target bucket;
-//        refine (exact min/max of that bucket, then re-histogram; falls back to order-preserving
-//        integer keys when the value range degenerates) until <= kCap candidates remain;
-//        rank the candidates directly.  Every bucket map is monotone in d, so a candidate set is
-//        always a contiguous run of the sorted order and the result is exact with ties.
-//   5. L = tau + sum_{d<tau} (d - tau) / (alpha N)             lower-tail mean = -CVaR_alpha(-d)
-//      (= (sum of the m smallest + (alpha N - m) tau) / (alpha N); deterministic block reduction)
+//   3. d_i = h . xi_i                                           core/risk_metrics.py:145,233
+//   4. exact (m+1)-th order statistic tau of d, m = floor(alpha*N), sort-free: histogram of d in
+//      LDS over [mean_d - 5 sd_d, mean_d + 5 sd_d] (clamped, so every map is monotone in d)
+//                                                                         [barrier 2]
+//      every wave scans the histogram -> target bucket; when it holds <= kCap samples (the normal
+//      case) they are compacted per wave in a fixed order                 [barrier 3]
+//      and wave 0 ranks them directly.  Otherwise the bucket is refined (exact min/max, re-histogram;
+//      value-linear, then order-preserving integer keys) until <= kCap remain.  Because each map is
+//      monotone, a candidate set is always a contiguous run of the sorted order: exact with ties.
+//   5. L = tau + sum_{d<tau} (d - tau) / (alpha N)               lower-tail mean = -CVaR_alpha(-d)
+//      (= (sum of the m smallest + (alpha N - m) tau) / (alpha N)); the tail sum is accumulated
+//      relative to mean_d during the compaction pass, so no further reduction is needed.
 //   6. g_cvar = r - delta - L, g* = r - delta + eps/alpha - L, g~ = g* - r, r = R_c |h|
 //      (closed-form optimum of the LPs at core/risk_metrics.py:105-125 and :198-213;
 //       lambda* = 1/alpha because lambda only enters the budget row and its bound, :110,:122)
 //
-// No MFMA: ~6 flops per 16 B sample — the kernel is bounded by HBM.
-// All reductions have a fixed order, so results are bitwise reproducible run to run.
+// Wave reductions use DPP row permutations + readlane (no LDS round trips).  Every reduction and
+// the candidate order are fixed, so results are bitwise reproducible run to run.
+// No MFMA: ~10 flops per 16-B sample — the kernel is bounded by HBM.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -32,80 +37,120 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kCap = 128;          // candidate count ranked directly
-constexpr int kMaxValueIters = 3;  // value-linear passes before switching to integer keys
+constexpr int kCap = 128;          // candidates ranked directly (per-wave region size in LDS)
+constexpr int kMaxValueIters = 3;  // value-linear refinements before switching to integer keys
 constexpr double kSentinel = 100.0;
 
+#ifdef DRCVAR_STAMPS
+// diagnostic build only: per-unit shader-clock stamps at phase boundaries (wave 0)
+constexpr int kStampUnits = 16384, kStamps = 8;
+__device__ unsigned long long g_stamps[kStampUnits * kStamps];
+#define DRCVAR_STAMP(k)                                                                       \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < kStampUnits)                                         \
+      g_stamps[blockIdx.x * kStamps + (k)] = __builtin_amdgcn_s_memtime();                    \
+  } while (0)
+#else
+#define DRCVAR_STAMP(k) \
+  do {                  \
+  } while (0)
+#endif
+
+// Launch-uniform scalars, precomputed on the host so the per-unit critical path carries as few
+// fp64 divisions as possible.
 struct Params {
-  double rc;  // robot_radius + obstacle_radius
+  double rc;              // robot_radius + obstacle_radius
   double alpha;
   double delta;
   double epsilon;
+  double eps_over_alpha;  // lambda* epsilon (risk_metrics.py:110,122)
+  double inv_n;           // 1 / N
+  double inv_n0;          // 1 / min(N, threads per unit): row-0 subsample for the window
+  double k;               // alpha N
+  double inv_k;           // 1 / (alpha N)
+  double z_alpha;         // standard-normal alpha-quantile: centre of the fast-path window
+  double window_sd;       // half-width of the fast-path window, in sd of d
+  uint32_t rank;          // min(floor(alpha N), N - 1): 0-based rank of tau
+  int unbounded;          // alpha N > N: both LPs unbounded (tau -> -inf), solver-failure sentinel
+  double degenerate_sq;   // smallest x with sqrt(x) >= 1e-10: |v| < 1e-10  <=>  v.v < degenerate_sq
 };
 
-// ---------------------------------------------------------------------------------------------
-// wave / workgroup reductions (butterfly: every lane ends with the bitwise-identical value)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
-  return v;
+// 1/sqrt(x) to ~1 ulp: hardware seed + one Newton step (the exact sqrt + divide sequence is far
+// longer and sits on the critical path of every unit)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return y * fma(-0.5 * x * y, y, 1.5);
 }
 
-// Sum of three values over the workgroup; `slot` is LDS scratch of 3*NW doubles owned by this
-// call site (callers never reuse a slot without two barriers in between).
-template <int NW>
-__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* slot) {
-  a = wave_sum(a);
-  b = wave_sum(b);
-  c = wave_sum(c);
-  if constexpr (NW > 1) {
-    const int w = threadIdx.x / kWave;
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-      slot[w] = a;
-      slot[NW + w] = b;
-      slot[2 * NW + w] = c;
-    }
-    __syncthreads();
-    a = slot[0];
-    b = slot[NW];
-    c = slot[2 * NW];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) {
-      a += slot[i];
-      b += slot[NW + i];
-      c += slot[2 * NW + i];
-    }
-  }
+// ---------------------------------------------------------------------------------------------
+// wave primitives: DPP row permutations (each an involution, so every lane of a row ends with the
+// bitwise-identical value), then the four row results combined through readlane in fixed order
+// ---------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+constexpr int kDppQuadXor1 = 0xB1;    // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;    // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // row_half_mirror
+constexpr int kDppMirror = 0x140;     // row_mirror
+
+struct OpAdd {
+  __device__ static double f(double a, double b) { return a + b; }
+};
+struct OpMin {
+  __device__ static double f(double a, double b) { return fmin(a, b); }
+};
+struct OpMax {
+  __device__ static double f(double a, double b) { return fmax(a, b); }
+};
+
+// Result is uniform across the wave.  Requires all 64 lanes active.
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v) {
+  v = Op::f(v, dpp_f64<kDppQuadXor1>(v));
+  v = Op::f(v, dpp_f64<kDppQuadXor2>(v));
+  v = Op::f(v, dpp_f64<kDppHalfMirror>(v));
+  v = Op::f(v, dpp_f64<kDppMirror>(v));
+  return Op::f(Op::f(readlane_f64(v, 0), readlane_f64(v, 16)),
+               Op::f(readlane_f64(v, 32), readlane_f64(v, 48)));
 }
 
-template <int NW>
-__device__ __forceinline__ void block_minmax(double& mn, double& mx, double* slot) {
-  mn = wave_min(mn);
-  mx = wave_max(mx);
+template <class Op>
+__device__ __forceinline__ double identity_of();
+template <>
+__device__ __forceinline__ double identity_of<OpAdd>() { return 0.0; }
+template <>
+__device__ __forceinline__ double identity_of<OpMin>() { return INFINITY; }
+template <>
+__device__ __forceinline__ double identity_of<OpMax>() { return -INFINITY; }
+
+// Workgroup reduction of K values.  `slot` is LDS scratch of K*NW doubles owned by the call site
+// (never reused by another call without a barrier in between).  The per-wave partials are
+// combined by a second wave reduction (lane w holds wave w's partial), so the order is fixed.
+template <class Op, int NW, int K>
+__device__ __forceinline__ void block_reduce(double (&v)[K], double* slot) {
+#pragma unroll
+  for (int q = 0; q < K; ++q) v[q] = wave_reduce<Op>(v[q]);
   if constexpr (NW > 1) {
+    const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-      slot[w] = mn;
-      slot[NW + w] = mx;
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < K; ++q) slot[q * NW + w] = v[q];
     }
     __syncthreads();
-    mn = slot[0];
-    mx = slot[NW];
 #pragma unroll
-    for (int i = 1; i < NW; ++i) {
-      mn = fmin(mn, slot[i]);
-      mx = fmax(mx, slot[NW + i]);
+    for (int q = 0; q < K; ++q) {
+      const double part = lane < NW ? slot[q * NW + lane] : identity_of<Op>();
+      v[q] = wave_reduce<Op>(part);
     }
   }
 }
@@ -116,7 +161,7 @@ __device__ __forceinline__ uint64_t f64_key(double d) {
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
-// Monotone bucket map of the current candidate interval [lo, hi] onto NB bins.
+// Monotone (non-decreasing) map of the candidate interval [lo, hi] onto NB histogram bins.
 template <int LOG_NB>
 struct BucketMap {
   static constexpr int NB = 1 << LOG_NB;
@@ -125,60 +170,327 @@ struct BucketMap {
   uint64_t klo;
   int shift;
 
-  __device__ __forceinline__ void init(double lo_, double hi_, int iter) {
+  // exact range [lo_, hi_] of the candidates, lo_ < hi_: bucket(lo_) = 0 < bucket(hi_)
+  __device__ __forceinline__ void init_range(double lo_, double hi_, int iter) {
     lo = lo_;
     const double range = hi_ - lo_;
     scale = static_cast<double>(NB) / range;
-    // value-linear while the range is well-conditioned: bucket(lo) = 0 and bucket(hi) >= 1
     value_mode = iter < kMaxValueIters && range > 0.0 && scale < 1e300 && range * scale >= 1.0;
     klo = f64_key(lo_);
     const uint64_t diff = f64_key(hi_) - klo;  // >= 1 when hi > lo
     const int bits = 64 - __builtin_clzll(diff | 1ull);
     shift = bits > LOG_NB ? bits - LOG_NB : 0;
   }
-  // precondition: lo <= d <= hi
   __device__ __forceinline__ int operator()(double d) const {
     if (value_mode) {
-      const int b = static_cast<int>((d - lo) * scale);
-      return b < NB - 1 ? b : NB - 1;
+      const double t = fmin(fmax((d - lo) * scale, 0.0), static_cast<double>(NB - 1));
+      return static_cast<int>(t);
     }
-    return static_cast<int>((f64_key(d) - klo) >> shift);
+    return static_cast<int>((f64_key(d) - klo) >> shift);  // key mode: lo <= d <= hi only
   }
 };
 
-// Wave 0: find the bin holding the candidate of rank rr (0-based) of the histogram.
+struct ScanResult {
+  int bin;
+  uint32_t below, cnt;
+  bool found;  // false when the histogram holds fewer than rr + 1 samples
+};
+
+// Histogram storage: lane l of a scanning wave owns bins [l*B, (l+1)*B), B = NB/64.  One padding
+// word after every B bins makes the owner reads conflict-free (lane stride B+1 words, B+1 odd).
 template <int NB>
-__device__ __forceinline__ void scan_bins(const uint32_t* hist, uint32_t rr, int lane,
-                                          int* out_bin, uint32_t* out_below, uint32_t* out_cnt) {
+__device__ __forceinline__ int hist_slot(int bin) {
+  constexpr int B = NB / kWave;
+  return bin + bin / B;
+}
+template <int NB>
+constexpr int hist_words() {
+  return NB + kWave;
+}
+
+// Inclusive prefix sum over the 64 lanes: DPP row shifts within each row of 16, then the row
+// totals (lanes 15, 31, 47) added through readlane — no LDS round trips.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x, int lane) {
+  constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+  int v = static_cast<int>(x);
+  v += __builtin_amdgcn_update_dpp(0, v, kRowShr1, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, kRowShr2, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, kRowShr4, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, kRowShr8, 0xF, 0xF, true);
+  const int r0 = __builtin_amdgcn_readlane(v, 15);
+  const int r1 = __builtin_amdgcn_readlane(v, 31);
+  const int r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = lane >> 4;
+  v += (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+  return static_cast<uint32_t>(v);
+}
+
+// Any wave: the bin holding the sample of rank rr (0-based) and the counts below / inside it.
+// Result is uniform across the wave.
+template <int NB>
+__device__ __forceinline__ ScanResult scan_bins(const uint32_t* hist, uint32_t rr, int lane) {
   constexpr int B = NB / kWave;  // contiguous bins per lane
+  const uint32_t* mine = hist + lane * (B + 1);
+  uint32_t h[B];
   uint32_t s = 0;
 #pragma unroll
-  for (int q = 0; q < B; ++q) s += hist[lane * B + q];
-  uint32_t incl = s;
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const uint32_t v = __shfl_up(incl, off, kWave);
-    if (lane >= off) incl += v;
+  for (int q = 0; q < B; ++q) {
+    h[q] = mine[q];
+    s += h[q];
   }
+  const uint32_t incl = wave_inclusive_scan(s, lane);
   const unsigned long long hit = __ballot(incl > rr);
-  const int owner = __ffsll(static_cast<long long>(hit)) - 1;
-  if (lane == owner) {
-    uint32_t cum = incl - s;
-    for (int q = 0; q < B; ++q) {
-      const uint32_t h = hist[lane * B + q];
-      if (cum + h > rr) {
-        *out_bin = lane * B + q;
-        *out_below = cum;
-        *out_cnt = h;
-        break;
-      }
-      cum += h;
-    }
+  if (hit == 0ull) return ScanResult{0, 0u, 0u, false};
+  const int owner = __ffsll(static_cast<long long>(hit)) - 1;  // uniform
+  // in the owner lane: first bin whose running count passes rr (branch-free over the B bins)
+  uint32_t cum = incl - s;
+  int bin = lane * B + B - 1;
+  uint32_t below = 0, cnt = 0;
+  bool done = false;
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    const bool take = !done && cum + h[q] > rr;
+    bin = take ? lane * B + q : bin;
+    below = take ? cum : below;
+    cnt = take ? h[q] : cnt;
+    done = done || take;
+    cum += h[q];
   }
+  return ScanResult{__builtin_amdgcn_readlane(bin, owner),
+                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(below), owner)),
+                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), owner)),
+                    true};
 }
 
 __device__ __forceinline__ bool in_range(double d, double lo, double hi) {
   return lo <= d && d <= hi;  // false for the NaN padding of idle slots
+}
+
+// MeanSafeHalfspace (core/halfspaces.py:84-94): direction from the ORIGIN, offset
+// -(h.mu - R_c |h|), with compute_separating_vector's [1, 0] fallback
+__device__ __forceinline__ void mean_halfspace(double mux, double muy, double rc, double* m0,
+                                               double* m1, double* g) {
+  const double nm = sqrt(mux * mux + muy * muy);
+  const bool degenerate = nm < 1e-10;
+  *m0 = degenerate ? 1.0 : mux / nm;
+  *m1 = degenerate ? 0.0 : muy / nm;
+  *g = -((*m0 * mux + *m1 * muy) - rc * sqrt(*m0 * *m0 + *m1 * *m1));
+}
+
+// columns 0..2 of the record (the mean halfspace), by one lane
+__device__ __forceinline__ void write_mean_halfspace(double* rec, double mux, double muy,
+                                                     double rc, int lane) {
+  double m0, m1, g_mean;
+  mean_halfspace(mux, muy, rc, &m0, &m1, &g_mean);
+  if (lane == 0) {
+    reinterpret_cast<double2*>(rec)[0] = make_double2(m0, m1);
+    rec[DRCVAR_COL_G_MEAN] = g_mean;
+  }
+}
+
+__device__ __forceinline__ void store_record(double* rec, double m0, double m1, double gm,
+                                             double h0, double h1, double gc, double gs,
+                                             double gt) {
+  reinterpret_cast<double2*>(rec)[0] = make_double2(m0, m1);
+  reinterpret_cast<double2*>(rec)[1] = make_double2(gm, h0);
+  reinterpret_cast<double2*>(rec)[2] = make_double2(h1, gc);
+  reinterpret_cast<double2*>(rec)[3] = make_double2(gs, gt);
+}
+
+// d_i = h . xi_i — one expression, used both for the register-resident samples and for re-reads,
+// so both paths see bitwise-identical values (core/risk_metrics.py:145,233: h @ samples.T)
+__device__ __forceinline__ double project(double h0, double h1, double x, double y) {
+  return fma(h0, x, h1 * y);
+}
+
+template <bool VEC>
+__device__ __forceinline__ double project_at(const double* base, int i, int64_t s_samp, double h0,
+                                             double h1) {
+  const int64_t off = static_cast<int64_t>(i) * s_samp;
+  if constexpr (VEC) {
+    const double2 v = *reinterpret_cast<const double2*>(base + off);
+    return project(h0, h1, v.x, v.y);
+  } else {
+    return project(h0, h1, base[off], base[off + 1]);
+  }
+}
+
+// Value-linear bucket map of the fast-path window [lo, lo + NB/scale]: monotone for any
+// scale > 0.  Values below the window map to bins <= 0, values above (and the +inf padding) to
+// NB - 1; callers test window membership separately where it matters.
+template <int NB>
+struct LinearMap {
+  double lo, scale;
+  __device__ __forceinline__ int operator()(double d) const {
+    const int b = static_cast<int>(fmin((d - lo) * scale, static_cast<double>(NB - 1)));
+    return b;
+  }
+};
+
+// Per-wave ordered compaction step: append the candidates of one row to this wave's LDS region.
+__device__ __forceinline__ void append_candidate(double* region, uint32_t& wbase, bool is_cand,
+                                                 double v, unsigned long long lt_mask) {
+  const unsigned long long ballot = __ballot(is_cand);
+  if (is_cand) region[wbase + __popcll(ballot & lt_mask)] = v;
+  wbase += static_cast<uint32_t>(__popcll(ballot));
+}
+
+// Wave 0 (all lanes active): tau = the candidate of rank rr among the c <= kCap candidates held in
+// per-wave regions cand[w * kCap + i], i < wcount[w] (global order: wave, then position — fixed).
+// Candidates are pulled into registers (g = lane, lane + 64) and compared through readlane, so
+// the O(c^2) ranking never waits on LDS.  Also returns s_cand = sum over candidates below tau of
+// (cand - tau), reduced in fixed order.
+template <int NW>
+__device__ __forceinline__ double rank_candidates(const double* cand, const uint32_t* wcount,
+                                                  uint32_t c, uint32_t rr, int lane,
+                                                  double* s_cand) {
+  const uint32_t cw = lane < NW ? wcount[lane] : 0u;  // lane w < NW: count of wave w
+  int slot[2] = {-1, -1};
+  uint32_t acc = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const uint32_t nw = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cw), w));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t g = lane + q * kWave;
+      if (g >= acc && g < acc + nw) slot[q] = w * kCap + static_cast<int>(g - acc);
+    }
+    acc += nw;
+  }
+  double mine[2] = {NAN, NAN};  // candidates g = lane, lane + 64
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    if (slot[q] >= 0) mine[q] = cand[slot[q]];
+  uint32_t less[2] = {0u, 0u}, eq[2] = {0u, 0u};
+  const uint32_t c0 = c < kWave ? c : kWave;
+  for (uint32_t i = 0; i < c0; ++i) {  // uniform trip count
+    const double z = readlane_f64(mine[0], static_cast<int>(i));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      less[q] += (z < mine[q]) ? 1u : 0u;
+      eq[q] += (z == mine[q]) ? 1u : 0u;
+    }
+  }
+  for (uint32_t i = kWave; i < c; ++i) {
+    const double z = readlane_f64(mine[1], static_cast<int>(i - kWave));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      less[q] += (z < mine[q]) ? 1u : 0u;
+      eq[q] += (z == mine[q]) ? 1u : 0u;
+    }
+  }
+  bool found = false;
+  double found_v = 0.0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (lane + q * kWave < c && less[q] <= rr && rr < less[q] + eq[q]) {
+      found = true;
+      found_v = mine[q];
+    }
+  }
+  const unsigned long long fb = __ballot(found);
+  const double tau = readlane_f64(found_v, __ffsll(static_cast<long long>(fb)) - 1);
+  double part = 0.0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    if (mine[q] < tau) part += mine[q] - tau;
+  *s_cand = wave_reduce<OpAdd>(part);
+  return tau;
+}
+
+// Exact selection for the units the register fast path does not finish (degenerate moments, or a
+// first-pass bucket with more than kCap samples).  It re-reads the unit's samples (L2/MALL-hot)
+// instead of keeping register state live: exact min/max, then histogram refinement (value-linear,
+// then order-preserving integer keys) until <= kCap candidates remain or the run collapses to one
+// value.  Result (valid in wave 0): tau and dsum = sum_{d<tau} (d - tau).
+template <int BLOCK, int LOG_NB, bool VEC>
+__device__ __forceinline__ void select_from_memory(const double* base, int n, int64_t s_samp,
+                                                double h0, double h1, double mu_d, uint32_t rank,
+                                                uint32_t* hist, double* cand, uint32_t* wcount,
+                                                double* red_rng, double* red_tail, double* tau_out,
+                                                double* dsum_out) {
+  constexpr int NW = BLOCK / kWave;
+  constexpr int NB = 1 << LOG_NB;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = tid / kWave;
+  __syncthreads();  // the fast path's readers of hist / red_* are done
+
+  double vmin[1] = {INFINITY}, vmax[1] = {-INFINITY};
+  for (int i = tid; i < n; i += BLOCK) {
+    const double v = project_at<VEC>(base, i, s_samp, h0, h1);
+    vmin[0] = fmin(vmin[0], v);
+    vmax[0] = fmax(vmax[0], v);
+  }
+  block_reduce<OpMin, NW, 1>(vmin, red_rng);
+  block_reduce<OpMax, NW, 1>(vmax, red_rng + NW);
+  double lo = vmin[0], hi = vmax[0];
+  uint32_t rr = rank, c = static_cast<uint32_t>(n);
+  bool have_bin = false, tau_known = lo == hi;
+  double tau = lo;
+  int bin = 0;
+  BucketMap<LOG_NB> map;
+  for (int iter = 0; !tau_known; ++iter) {
+    map.init_range(lo, hi, iter);
+    for (int b = tid; b < hist_words<NB>(); b += BLOCK) hist[b] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += BLOCK) {
+      const double v = project_at<VEC>(base, i, s_samp, h0, h1);
+      if (in_range(v, lo, hi)) atomicAdd(&hist[hist_slot<NB>(map(v))], 1u);
+    }
+    __syncthreads();
+    const ScanResult sr = scan_bins<NB>(hist, rr, lane);
+    bin = sr.bin;
+    rr -= sr.below;
+    c = sr.cnt;
+    have_bin = true;
+    if (c <= kCap) break;
+    double rmin[1] = {INFINITY}, rmax[1] = {-INFINITY};
+    for (int i = tid; i < n; i += BLOCK) {
+      const double v = project_at<VEC>(base, i, s_samp, h0, h1);
+      if (in_range(v, lo, hi) && map(v) == bin) {
+        rmin[0] = fmin(rmin[0], v);
+        rmax[0] = fmax(rmax[0], v);
+      }
+    }
+    __syncthreads();  // all waves have scanned hist before it is cleared again
+    block_reduce<OpMin, NW, 1>(rmin, red_rng);
+    block_reduce<OpMax, NW, 1>(rmax, red_rng + NW);
+    lo = rmin[0];
+    hi = rmax[0];
+    have_bin = false;
+    if (lo == hi) {
+      tau_known = true;
+      tau = lo;
+    }
+  }
+
+  double sq = 0.0;
+  uint32_t wbase = 0;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  for (int i0 = 0; i0 < n; i0 += BLOCK) {  // uniform trip count: ballots see whole waves
+    const int i = i0 + tid;
+    const double v = i < n ? project_at<VEC>(base, i, s_samp, h0, h1) : NAN;
+    const bool inr = in_range(v, lo, hi);
+    const int bj = (have_bin && inr) ? map(v) : 0;
+    const bool below = v < lo || (have_bin && inr && bj < bin);
+    if (below) sq += v - mu_d;
+    append_candidate(cand + wave * kCap, wbase, !tau_known && inr && (!have_bin || bj == bin), v,
+                     lt_mask);
+  }
+  sq = wave_reduce<OpAdd>(sq);
+  if (lane == 0) {
+    red_tail[wave] = sq;
+    wcount[wave] = wbase;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const double s_below = wave_reduce<OpAdd>(lane < NW ? red_tail[lane] : 0.0);
+  double s_cand = 0.0;
+  if (!tau_known) tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
+  const double n_below = static_cast<double>(rank - rr);
+  *tau_out = tau;
+  *dsum_out = (s_below - n_below * (tau - mu_d)) + s_cand;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -191,229 +503,266 @@ __device__ __forceinline__ bool in_range(double d, double lo, double hi) {
 // ---------------------------------------------------------------------------------------------
 template <int BLOCK, int P, int LOG_NB, bool VEC, bool GIVEN_H>
 __global__ void __launch_bounds__(BLOCK)
-safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int64_t n,
+safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
                       int64_t s_obs, int64_t s_step, int64_t s_samp,
                       const double* __restrict__ dir, int64_t dir_s_obs, int64_t dir_s_step,
                       Params prm, double* __restrict__ out) {
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << LOG_NB;
-  __shared__ uint32_t hist[NB];
-  __shared__ double cand[kCap];
-  __shared__ double red_sum[3 * NW];
+  __shared__ uint32_t hist[hist_words<NB>()];
+  __shared__ double cand[NW * kCap];
+  __shared__ uint32_t wcount[NW];
+  __shared__ uint32_t wbelow_sh[NW];
+  __shared__ double red_mom[7 * NW];
   __shared__ double red_rng[2 * NW];
-  __shared__ double red_ref[2 * NW];
-  __shared__ double red_tail[3 * NW];
-  __shared__ int sh_bin;
-  __shared__ uint32_t sh_below, sh_cnt, sh_ncand;
-  __shared__ double sh_tau;
+  __shared__ double red_tail[NW];
 
   const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = tid / kWave;
   const int64_t u = blockIdx.x;
   const int64_t o = u / n_steps;
   const int64_t t = u - o * n_steps;
   const double* base = samples + o * s_obs + t * s_step;
-  if (tid == 0) sh_ncand = 0;
+  double* rec = out + u * DRCVAR_OUT_WIDTH;
 
-  // ---- 1. load + sum ---------------------------------------------------------------------
+  DRCVAR_STAMP(0);
+#if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 0
+  if (tid == 0) rec[0] = 0.0;  // diagnostic build: dispatch cost only
+  return;
+#endif
+#pragma unroll
+  for (int b = tid; b < hist_words<NB>(); b += BLOCK) hist[b] = 0u;
+
+  // ---- 1. load + moments ----------------------------------------------------------------
+  // Branch-free: idle slots of the last row re-load sample n-1 and contribute zeros.
   double x[P], y[P];
-  double sx = 0.0, sy = 0.0, bad = 0.0;
 #pragma unroll
   for (int j = 0; j < P; ++j) {
-    const int64_t i = tid + static_cast<int64_t>(j) * BLOCK;
-    if (i < n) {
-      if constexpr (VEC) {
-        const double2 v = *reinterpret_cast<const double2*>(base + i * s_samp);
-        x[j] = v.x;
-        y[j] = v.y;
-      } else {
-        x[j] = base[i * s_samp];
-        y[j] = base[i * s_samp + 1];
-      }
-      sx += x[j];
-      sy += y[j];
-      bad += (std::isfinite(x[j]) && std::isfinite(y[j])) ? 0.0 : 1.0;
+    const int i = tid + j * BLOCK;
+    const int64_t off = static_cast<int64_t>(i < n ? i : n - 1) * s_samp;
+    if constexpr (VEC) {
+      const double2 v = *reinterpret_cast<const double2*>(base + off);
+      x[j] = v.x;
+      y[j] = v.y;
     } else {
-      x[j] = 0.0;
-      y[j] = 0.0;
+      x[j] = base[off];
+      y[j] = base[off + 1];
     }
   }
-  block_sum3<NW>(sx, sy, bad, red_sum);
-  const double dn = static_cast<double>(n);
-  const double mux = sx / dn, muy = sy / dn;
+  // Sums for the mean over every sample (plain sums, as np.mean); second moments over row 0 only
+  // (the first BLOCK samples) — they merely position the fast-path window, so a subsample is
+  // enough and cancellation in them can only cost speed, never exactness.
+  double mom[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // Sx Sy | Sx0 Sy0 Sxx0 Syy0 Sxy0
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const bool valid = tid + j * BLOCK < n;
+    const double a = valid ? x[j] : 0.0, b = valid ? y[j] : 0.0;
+    mom[0] += a;
+    mom[1] += b;
+    if (j == 0) {
+      mom[2] = a;
+      mom[3] = b;
+      mom[4] = a * a;
+      mom[5] = b * b;
+      mom[6] = a * b;
+    }
+  }
+  DRCVAR_STAMP(1);
+  block_reduce<OpAdd, NW, 7>(mom, red_mom);                              // [barrier 1]
+  DRCVAR_STAMP(2);
+  const double mux = mom[0] * prm.inv_n, muy = mom[1] * prm.inv_n;
+  // any non-finite sample makes a sum non-finite (so do sums that overflow): solver failure
+  const bool bad = !(std::isfinite(mom[0]) && std::isfinite(mom[1]));
+#if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 1
+  if (tid == 0) rec[0] = mux + muy + mom[2] + mom[3] + mom[4] + mom[5];  // diagnostic: load+moments
+  return;
+#endif
 
-  // ---- 2. directions ---------------------------------------------------------------------
+  // ---- 2. direction ----------------------------------------------------------------------
   const double* dp = dir + o * dir_s_obs + t * dir_s_step;
   double h0, h1;
   if constexpr (GIVEN_H) {
     h0 = dp[0];
     h1 = dp[1];
-  } else {
+  } else {  // compute_separating_vector(ego, mu), core/geometry.py:35-53
     const double dx = mux - dp[0], dy = muy - dp[1];
-    const double nrm = sqrt(dx * dx + dy * dy);
-    h0 = 1.0;
-    h1 = 0.0;
-    if (!(nrm < 1e-10)) {
-      h0 = dx / nrm;
-      h1 = dy / nrm;
-    }
+    const double n2 = dx * dx + dy * dy;
+    const double inv = std::isfinite(n2) ? rsqrt_nr(n2) : 1.0 / sqrt(n2);  // inf: as diff/norm
+    const bool degenerate = n2 < prm.degenerate_sq;  // |mu - ego| < 1e-10 -> [1, 0]
+    h0 = degenerate ? 1.0 : dx * inv;
+    h1 = degenerate ? 0.0 : dy * inv;
   }
-  const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);
-  double* rec = out + u * DRCVAR_OUT_WIDTH;
-  if (tid == 0) {
-    const double nm = sqrt(mux * mux + muy * muy);
-    double m0 = 1.0, m1 = 0.0;
-    if (!(nm < 1e-10)) {
-      m0 = mux / nm;
-      m1 = muy / nm;
-    }
-    rec[DRCVAR_COL_MEAN_H0] = m0;
-    rec[DRCVAR_COL_MEAN_H1] = m1;
-    rec[DRCVAR_COL_G_MEAN] = -((m0 * mux + m1 * muy) - prm.rc * sqrt(m0 * m0 + m1 * m1));
-    rec[DRCVAR_COL_H0] = h0;
-    rec[DRCVAR_COL_H1] = h1;
-  }
-  const double k = prm.alpha * dn;
-  if (bad != 0.0 || !(k <= dn)) {  // solver-failure convention, risk_metrics.py:298-303,334-338
+  if (bad || prm.unbounded) {  // solver failure, risk_metrics.py:298-303,334-338
     if (tid == 0) {
-      rec[DRCVAR_COL_G_CVAR] = kSentinel;
-      rec[DRCVAR_COL_G_DR_STAR] = kSentinel;
-      rec[DRCVAR_COL_G_DR_TILDE] = kSentinel - r;
+      const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);
+      double m0, m1, g_mean;
+      mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
+      store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
     }
     return;  // uniform across the workgroup
   }
 
-  // ---- 3. projections --------------------------------------------------------------------
+  // ---- 3. projections; window histogram around the estimated quantile ------------------------
   double d[P];
-  double dmin = INFINITY, dmax = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < P; ++j) {
-    const int64_t i = tid + static_cast<int64_t>(j) * BLOCK;
-    d[j] = (i < n) ? h0 * x[j] + h1 * y[j] : NAN;
-    if (i < n) {
-      dmin = fmin(dmin, d[j]);
-      dmax = fmax(dmax, d[j]);
+  for (int j = 0; j < P; ++j)  // +inf padding: never below, inside or a candidate
+    d[j] = (tid + j * BLOCK < n) ? project(h0, h1, x[j], y[j]) : INFINITY;
+  const double mu_d = h0 * mux + h1 * muy;
+  const double ma0 = mom[2] * prm.inv_n0, mb0 = mom[3] * prm.inv_n0;  // row-0 covariance
+  const double cxx = mom[4] * prm.inv_n0 - ma0 * ma0, cyy = mom[5] * prm.inv_n0 - mb0 * mb0;
+  const double cxy = mom[6] * prm.inv_n0 - ma0 * mb0;
+  const double var_d = h0 * h0 * cxx + 2.0 * h0 * h1 * cxy + h1 * h1 * cyy;
+  // window [wlo, whi] = mean_d + (z_alpha -+ window_sd) sd_d; only samples inside it are
+  // histogrammed (LDS atomics), samples below it are counted with ballots.  Any positive scale
+  // keeps the map monotone, so the approximate reciprocal square root is exact enough.
+  const double inv_sd = rsqrt_nr(var_d);
+  const double sd_d = var_d * inv_sd;
+  const double wlo = mu_d + (prm.z_alpha - prm.window_sd) * sd_d;
+  const double whi = mu_d + (prm.z_alpha + prm.window_sd) * sd_d;
+  const LinearMap<NB> map{wlo, static_cast<double>(NB) / (2.0 * prm.window_sd) * inv_sd};
+  const uint32_t rank = prm.rank;
+  bool fast = var_d > 0.0 && std::isfinite(map.scale) && std::isfinite(wlo) && map.scale > 0.0;
+  uint32_t rr = rank, c = 0;
+  int bin = 0;
+  // per-sample bucket codes, two 16-bit codes per register: the bin inside the window, 0xFFFF
+  // outside it (the sum of samples below the window is taken in this pass)
+  constexpr int PC = (P + 1) / 2;
+  uint32_t code[PC];
+  double sq = 0.0;  // sum over samples below the target bucket of (d - mu_d)
+  if (fast) {
+    uint32_t wbelow = 0;  // samples of this wave below the window (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const double v = d[j];
+      const bool low = v < wlo;
+      wbelow += static_cast<uint32_t>(__popcll(__ballot(low)));
+      sq += low ? v - mu_d : 0.0;
+      const bool inw = !low && v <= whi;
+      const int b = map(v);
+      if (inw) atomicAdd(&hist[hist_slot<NB>(b)], 1u);
+      const uint32_t cj = inw ? static_cast<uint32_t>(b) : 0xFFFFu;
+      if (j % 2 == 0) code[j / 2] = cj;
+      else code[j / 2] |= cj << 16;
     }
-  }
-  block_minmax<NW>(dmin, dmax, red_rng);
-
-  // ---- 4. exact order statistic ----------------------------------------------------------
-  const int64_t m = static_cast<int64_t>(floor(k));
-  const uint32_t rank = static_cast<uint32_t>(m < n - 1 ? m : n - 1);
-  double tau;
-  if (dmin == dmax) {
-    tau = dmin;
-  } else {
-    double lo = dmin, hi = dmax;
-    uint32_t rr = rank;                      // rank inside the candidate set
-    uint32_t c = static_cast<uint32_t>(n);  // candidate count
-    bool have_bin = false;                   // candidates = bucket `bin` of `map` within [lo, hi]
-    int bin = 0;
-    BucketMap<LOG_NB> map;
-    for (int iter = 0; c > kCap; ++iter) {
-      if (have_bin) {  // shrink [lo, hi] to the exact range of the target bucket
-        double mn = INFINITY, mx = -INFINITY;
+    if (lane == 0) wbelow_sh[wave] = wbelow;
+    DRCVAR_STAMP(3);
+    __syncthreads();                                                      // [barrier 2]
+    uint32_t below = 0;  // all samples below the window
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-          if (in_range(d[j], lo, hi) && map(d[j]) == bin) {
-            mn = fmin(mn, d[j]);
-            mx = fmax(mx, d[j]);
-          }
-        }
-        block_minmax<NW>(mn, mx, red_ref);
-        lo = mn;
-        hi = mx;
-        have_bin = false;
-        if (lo == hi) break;
-      }
-      map.init(lo, hi, iter);
-      for (int b = tid; b < NB; b += BLOCK) hist[b] = 0u;
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < P; ++j) {
-        if (in_range(d[j], lo, hi)) atomicAdd(&hist[map(d[j])], 1u);
-      }
-      __syncthreads();
-      if (tid < kWave) scan_bins<NB>(hist, rr, tid, &sh_bin, &sh_below, &sh_cnt);
-      __syncthreads();
-      bin = sh_bin;
-      rr -= sh_below;
-      c = sh_cnt;
-      have_bin = true;
-    }
-    if (!have_bin && lo == hi) {
-      tau = lo;
+    for (int w = 0; w < NW; ++w) below += wbelow_sh[w];
+    if (rank >= below) {
+      const ScanResult sr = scan_bins<NB>(hist, rank - below, lane);     // every wave, same result
+      bin = sr.bin;
+      rr = rank - below - sr.below;
+      c = sr.cnt;
+      fast = sr.found && c <= kCap;
     } else {
-      // compact the <= kCap candidates into LDS and rank them directly
+      fast = false;  // tau lies below the window (far from Gaussian): exact fallback
+    }
+    DRCVAR_STAMP(4);
+  }
+#if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 2
+  if (tid == 0) rec[0] = static_cast<double>(bin) + c + rr;  // diagnostic: + histogram and scan
+  return;
+#endif
+
+  // ---- 4. candidates of the target bucket + tail sum below them -----------------------------
+  double tau, dsum;  // dsum = sum_{d<tau} (d - tau)
+  if (fast) [[likely]] {
+    uint32_t wbase = 0;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    const uint32_t ubin = static_cast<uint32_t>(bin);
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        if (in_range(d[j], lo, hi) && (!have_bin || map(d[j]) == bin)) {
-          cand[atomicAdd(&sh_ncand, 1u)] = d[j];
-        }
-      }
-      __syncthreads();
-      for (uint32_t a = tid; a < c; a += BLOCK) {
-        const double v = cand[a];
-        uint32_t less = 0, eq = 0;
-        for (uint32_t b = 0; b < c; ++b) {
-          const double w = cand[b];
-          less += (w < v) ? 1u : 0u;
-          eq += (w == v) ? 1u : 0u;
-        }
-        if (less <= rr && rr < less + eq) sh_tau = v;  // ties write the same value
-      }
-      __syncthreads();
-      tau = sh_tau;
+    for (int j = 0; j < P; ++j) {
+      const uint32_t cj = (code[j / 2] >> (16 * (j % 2))) & 0xFFFFu;
+      sq += cj < ubin ? d[j] - mu_d : 0.0;
+      append_candidate(cand + wave * kCap, wbase, cj == ubin, d[j], lt_mask);
+    }
+    sq = wave_reduce<OpAdd>(sq);
+    if (lane == 0) {
+      red_tail[wave] = sq;
+      wcount[wave] = wbase;
+    }
+    DRCVAR_STAMP(5);
+    __syncthreads();                                                      // [barrier 3]
+    DRCVAR_STAMP(6);
+    if (wave != 0) {
+      if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
+      return;
+    }
+    const double s_below = wave_reduce<OpAdd>(lane < NW ? red_tail[lane] : 0.0);
+    double s_cand;
+    tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
+    dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
+  } else [[unlikely]] {
+    select_from_memory<BLOCK, LOG_NB, VEC>(base, n, s_samp, h0, h1, mu_d, rank, hist, cand,
+                                           wcount, red_rng, red_tail, &tau, &dsum);
+    if (wave != 0) {
+      if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
+      return;
     }
   }
 
-  // ---- 5. lower-tail sum, relative to tau -------------------------------------------------
-  // S_m = sum_{d<tau} d + (m - #{d<tau}) tau  and  L = (S_m + (k - m) tau) / k  simplify to
-  // L = tau + D / k  with  D = sum_{d<tau} (d - tau) <= 0: the differences are small, so the sum
-  // carries far less rounding than the plain tail sum when |d| >> spread.
-  double dsum = 0.0, unused0 = 0.0, unused1 = 0.0;
-#pragma unroll
-  for (int j = 0; j < P; ++j) {
-    if (d[j] < tau) dsum += d[j] - tau;
-  }
-  block_sum3<NW>(dsum, unused0, unused1, red_tail);
-
-  // ---- 6. offsets -------------------------------------------------------------------------
-  if (tid == 0) {
-    const double L = tau + dsum / k;
-    rec[DRCVAR_COL_G_CVAR] = r - prm.delta - L;
-    if (prm.epsilon >= 0.0) {
-      const double g_star = r - prm.delta + prm.epsilon / prm.alpha - L;
-      rec[DRCVAR_COL_G_DR_STAR] = g_star;
-      rec[DRCVAR_COL_G_DR_TILDE] = g_star - r;
-    } else {  // DR LP unbounded (lambda -> inf): solver-failure sentinel
-      rec[DRCVAR_COL_G_DR_STAR] = kSentinel;
-      rec[DRCVAR_COL_G_DR_TILDE] = kSentinel - r;
+  // ---- 5. offsets (wave 0) -------------------------------------------------------------------
+  const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);  // R_c |h| (risk_metrics.py:293, :234)
+  if (lane == 0) {
+    const double L = tau + dsum * prm.inv_k;  // lower-tail mean
+    const double g_cvar = r - prm.delta - L;
+    double g_star = kSentinel, g_tilde = kSentinel - r;
+    if (prm.epsilon >= 0.0) {  // else: DR LP unbounded (lambda -> inf), solver-failure sentinel
+      g_star = r - prm.delta + prm.eps_over_alpha - L;
+      g_tilde = g_star - r;
+    }
+    if constexpr (NW == 1) {
+      double m0, m1, g_mean;
+      mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
+      store_record(rec, m0, m1, g_mean, h0, h1, g_cvar, g_star, g_tilde);
+    } else {  // columns 0..2 are written by wave 1 (below)
+      reinterpret_cast<double*>(rec)[DRCVAR_COL_H0] = h0;
+      reinterpret_cast<double2*>(rec)[2] = make_double2(h1, g_cvar);
+      reinterpret_cast<double2*>(rec)[3] = make_double2(g_star, g_tilde);
     }
   }
+  DRCVAR_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------------------------
-// launch plans: smallest plan whose BLOCK * P covers N
+// launch plans
 // ---------------------------------------------------------------------------------------------
 struct Plan {
   int block, per, log_nb;
+  bool automatic;  // part of the default chain (smallest automatic plan with block*per >= N)
 };
 constexpr Plan kPlans[] = {
-    {64, 2, 7},      // N <=   128
-    {128, 4, 8},     // N <=   512
-    {256, 4, 9},     // N <=  1024
-    {256, 8, 10},    // N <=  2048
-    {256, 16, 11},   // N <=  4096
-    {512, 16, 12},   // N <=  8192
-    {1024, 10, 12},  // N <= 10240
-    {1024, 12, 12},  // N <= 12288
-    {1024, 16, 12},  // N <= 16384
+    {64, 2, 7, true},       // N <=   128
+    {128, 4, 8, true},      // N <=   512
+    {256, 4, 9, true},      // N <=  1024
+    {256, 8, 10, true},     // N <=  2048
+    {256, 16, 10, true},    // N <=  4096
+    {512, 16, 10, true},    // N <=  8192   (2 workgroups per CU)
+    {512, 20, 10, true},    // N <= 10240   (2 workgroups per CU)
+    {1024, 12, 10, true},   // N <= 12288
+    {1024, 16, 10, true},   // N <= 16384
+    // alternative geometries, selectable through drcvar_safe_halfspaces_f64_ex (tuning)
+    {64, 16, 9, false},
+    {128, 8, 9, false},
+    {512, 2, 9, false},
+    {1024, 10, 10, false},
+    {256, 20, 10, false},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
 
-int pick_plan(int64_t n) {
-  for (int p = 0; p < kNumPlans; ++p)
-    if (n <= static_cast<int64_t>(kPlans[p].block) * kPlans[p].per) return p;
+int pick_plan(int64_t n, int threads, int per) {
+  for (int p = 0; p < kNumPlans; ++p) {
+    const Plan& pl = kPlans[p];
+    if (n > static_cast<int64_t>(pl.block) * pl.per) continue;
+    if (threads == 0 && per == 0) {
+      if (pl.automatic) return p;
+    } else if (pl.block == threads && pl.per == per) {
+      return p;
+    }
+  }
   return -1;
 }
 
@@ -428,23 +777,24 @@ struct Launch {
 };
 
 template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
-void launch_plan(const Launch& L, bool vec) {
+void launch_plan(Launch L, bool vec) {
   const dim3 grid(static_cast<unsigned>(L.units)), block(BLOCK);
+  L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < BLOCK ? L.n : BLOCK);
   if (vec) {
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, true, GIVEN_H>), grid, block, 0,
-                       L.stream, L.samples, L.n_steps, L.n, L.s_obs, L.s_step, L.s_samp, L.dir,
+                       L.stream, L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
                        L.dir_s_obs, L.dir_s_step, L.prm, L.out);
   } else {
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, false, GIVEN_H>), grid, block, 0,
-                       L.stream, L.samples, L.n_steps, L.n, L.s_obs, L.s_step, L.s_samp, L.dir,
+                       L.stream, L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
                        L.dir_s_obs, L.dir_s_step, L.prm, L.out);
   }
 }
 
 template <bool GIVEN_H>
-int dispatch(const Launch& L) {
+int dispatch(const Launch& L, int threads, int per) {
   if (L.units == 0) return DRCVAR_OK;
-  const int p = pick_plan(L.n);
+  const int p = pick_plan(L.n, threads, per);
   if (p < 0) return DRCVAR_ERR_UNSUPPORTED;
   const bool vec = (reinterpret_cast<uintptr_t>(L.samples) % 16 == 0) && (L.s_obs % 2 == 0) &&
                    (L.s_step % 2 == 0) && (L.s_samp % 2 == 0);
@@ -454,13 +804,69 @@ int dispatch(const Launch& L) {
     case 1: launch_plan<128, 4, 8, GIVEN_H>(L, vec); break;
     case 2: launch_plan<256, 4, 9, GIVEN_H>(L, vec); break;
     case 3: launch_plan<256, 8, 10, GIVEN_H>(L, vec); break;
-    case 4: launch_plan<256, 16, 11, GIVEN_H>(L, vec); break;
-    case 5: launch_plan<512, 16, 12, GIVEN_H>(L, vec); break;
-    case 6: launch_plan<1024, 10, 12, GIVEN_H>(L, vec); break;
-    case 7: launch_plan<1024, 12, 12, GIVEN_H>(L, vec); break;
-    default: launch_plan<1024, 16, 12, GIVEN_H>(L, vec); break;
+    case 4: launch_plan<256, 16, 10, GIVEN_H>(L, vec); break;
+    case 5: launch_plan<512, 16, 10, GIVEN_H>(L, vec); break;
+    case 6: launch_plan<512, 20, 10, GIVEN_H>(L, vec); break;
+    case 7: launch_plan<1024, 12, 10, GIVEN_H>(L, vec); break;
+    case 8: launch_plan<1024, 16, 10, GIVEN_H>(L, vec); break;
+    case 9: launch_plan<64, 16, 9, GIVEN_H>(L, vec); break;
+    case 10: launch_plan<128, 8, 9, GIVEN_H>(L, vec); break;
+    case 11: launch_plan<512, 2, 9, GIVEN_H>(L, vec); break;
+    case 12: launch_plan<1024, 10, 10, GIVEN_H>(L, vec); break;
+    default: launch_plan<256, 20, 10, GIVEN_H>(L, vec); break;
   }
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
+}
+
+// Standard-normal quantile (P. J. Acklam's rational approximation, |rel err| < 1.2e-9) — only
+// positions the fast-path window, so its accuracy never affects results.
+double normal_quantile(double p) {
+  static const double a[] = {-3.969683028665376e+01, 2.209460984245205e+02, -2.759285104469687e+02,
+                             1.383577518672690e+02, -3.066479806614716e+01, 2.506628277459239e+00};
+  static const double b[] = {-5.447609879822406e+01, 1.615858368580409e+02, -1.556989798598866e+02,
+                             6.680131188771972e+01, -1.328068155288572e+01};
+  static const double c[] = {-7.784894002430293e-03, -3.223964580411365e-01, -2.400758277161838e+00,
+                             -2.549732539343734e+00, 4.374664141464968e+00, 2.938163982698783e+00};
+  static const double d[] = {7.784695709041462e-03, 3.224671290700398e-01, 2.445134137142996e+00,
+                             3.754408661907416e+00};
+  p = std::fmin(std::fmax(p, 1e-12), 1.0 - 1e-12);
+  const double plow = 0.02425;
+  if (p < plow) {
+    const double q = std::sqrt(-2.0 * std::log(p));
+    return (((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+           ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1.0);
+  }
+  if (p > 1.0 - plow) return -normal_quantile(1.0 - p);
+  const double q = p - 0.5, r = q * q;
+  return (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
+         (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1.0);
+}
+
+Params make_params(double rr, double ro, double alpha, double delta, double eps, int64_t n) {
+  Params p;
+  p.rc = rr + ro;
+  p.alpha = alpha;
+  p.delta = delta;
+  p.epsilon = eps;
+  p.eps_over_alpha = eps / alpha;
+  const double dn = static_cast<double>(n);
+  p.inv_n = 1.0 / dn;
+  p.k = alpha * dn;                      // exactly as the reference forms alpha * n_samples
+  p.inv_k = 1.0 / p.k;
+  p.unbounded = !(p.k <= dn);
+  const int64_t m = static_cast<int64_t>(std::floor(p.k));
+  p.rank = static_cast<uint32_t>(p.unbounded ? 0 : (m < n - 1 ? m : n - 1));
+  // window: the Gaussian alpha-quantile +- max(0.25 sd, 12 standard errors of the sample quantile)
+  const double a = std::fmin(std::fmax(alpha, 1e-12), 1.0 - 1e-12);
+  p.z_alpha = normal_quantile(a);
+  const double phi = std::exp(-0.5 * p.z_alpha * p.z_alpha) * 0.3989422804014327;
+  const double se = std::sqrt(a * (1.0 - a) / dn) / phi;
+  p.window_sd = std::fmax(0.25, 12.0 * se);
+  double t = 1e-20;  // smallest t with sqrt(t) >= 1e-10 (sqrt is correctly rounded and monotone)
+  while (std::sqrt(t) >= 1e-10) t = std::nextafter(t, 0.0);
+  while (std::sqrt(t) < 1e-10) t = std::nextafter(t, 1.0);
+  p.degenerate_sq = t;
+  return p;
 }
 
 bool params_ok(double rr, double ro, double alpha, double delta, double eps) {
@@ -468,9 +874,36 @@ bool params_ok(double rr, double ro, double alpha, double delta, double eps) {
          std::isfinite(delta) && std::isfinite(eps);
 }
 
+int safe_halfspaces(const double* samples, int64_t n_obstacles, int64_t n_steps,
+                    int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
+                    int64_t stride_sample, const double* ego_ref_pos, int64_t ego_stride_step,
+                    double robot_radius, double obstacle_radius, double alpha, double delta,
+                    double epsilon, double* out, void* stream, int threads, int per) {
+  if (n_obstacles < 0 || n_steps < 0 || n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (!params_ok(robot_radius, obstacle_radius, alpha, delta, epsilon))
+    return DRCVAR_ERR_INVALID_ARGUMENT;
+  const int64_t units = n_obstacles * n_steps;
+  if (units == 0) return DRCVAR_OK;
+  if (!samples || !ego_ref_pos || !out || units > 0x7fffffff) return DRCVAR_ERR_INVALID_ARGUMENT;
+  Launch L{samples, units, n_steps, n_samples, stride_obstacle, stride_step, stride_sample,
+           ego_ref_pos, 0, ego_stride_step,
+           make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
+           static_cast<hipStream_t>(stream)};
+  return dispatch<false>(L, threads, per);
+}
+
 }  // namespace
 
 extern "C" {
+
+#ifdef DRCVAR_STAMPS
+// diagnostic build only (not part of the ABI header): copy the phase stamps to the host
+int drcvar_diag_stamps(unsigned long long* host, int n_units) {
+  const int n = n_units < kStampUnits ? n_units : kStampUnits;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n * kStamps,
+                             0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
+#endif
 
 int drcvar_abi_version(void) { return DRCVAR_ABI_VERSION; }
 
@@ -478,7 +911,7 @@ const char* drcvar_strerror(int code) {
   switch (code) {
     case DRCVAR_OK: return "ok";
     case DRCVAR_ERR_INVALID_ARGUMENT: return "invalid argument";
-    case DRCVAR_ERR_UNSUPPORTED: return "n_samples exceeds DRCVAR_MAX_SAMPLES";
+    case DRCVAR_ERR_UNSUPPORTED: return "n_samples exceeds DRCVAR_MAX_SAMPLES or no such launch geometry";
     case DRCVAR_ERR_LAUNCH: return "HIP kernel launch failed";
     default: return "unknown error";
   }
@@ -487,7 +920,7 @@ const char* drcvar_strerror(int code) {
 int drcvar_launch_plan(int64_t n_samples, int32_t* threads_per_unit, int32_t* samples_per_thread,
                        int32_t* bins) {
   if (n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
-  const int p = pick_plan(n_samples);
+  const int p = pick_plan(n_samples, 0, 0);
   if (p < 0) return DRCVAR_ERR_UNSUPPORTED;
   if (threads_per_unit) *threads_per_unit = kPlans[p].block;
   if (samples_per_thread) *samples_per_thread = kPlans[p].per;
@@ -501,17 +934,23 @@ int drcvar_safe_halfspaces_f64(const double* samples, int64_t n_obstacles, int64
                                int64_t ego_stride_step, double robot_radius,
                                double obstacle_radius, double alpha, double delta, double epsilon,
                                double* out, void* stream) {
-  if (n_obstacles < 0 || n_steps < 0 || n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
-  if (!params_ok(robot_radius, obstacle_radius, alpha, delta, epsilon))
-    return DRCVAR_ERR_INVALID_ARGUMENT;
-  const int64_t units = n_obstacles * n_steps;
-  if (units == 0) return DRCVAR_OK;
-  if (!samples || !ego_ref_pos || !out || units > 0x7fffffff) return DRCVAR_ERR_INVALID_ARGUMENT;
-  Launch L{samples, units, n_steps, n_samples, stride_obstacle, stride_step, stride_sample,
-           ego_ref_pos, 0, ego_stride_step,
-           Params{robot_radius + obstacle_radius, alpha, delta, epsilon}, out,
-           static_cast<hipStream_t>(stream)};
-  return dispatch<false>(L);
+  return safe_halfspaces(samples, n_obstacles, n_steps, n_samples, stride_obstacle, stride_step,
+                         stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
+                         obstacle_radius, alpha, delta, epsilon, out, stream, 0, 0);
+}
+
+int drcvar_safe_halfspaces_f64_ex(const double* samples, int64_t n_obstacles, int64_t n_steps,
+                                  int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
+                                  int64_t stride_sample, const double* ego_ref_pos,
+                                  int64_t ego_stride_step, double robot_radius,
+                                  double obstacle_radius, double alpha, double delta,
+                                  double epsilon, double* out, void* stream,
+                                  int32_t threads_per_unit, int32_t samples_per_thread) {
+  if ((threads_per_unit == 0) != (samples_per_thread == 0)) return DRCVAR_ERR_INVALID_ARGUMENT;
+  return safe_halfspaces(samples, n_obstacles, n_steps, n_samples, stride_obstacle, stride_step,
+                         stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
+                         obstacle_radius, alpha, delta, epsilon, out, stream, threads_per_unit,
+                         samples_per_thread);
 }
 
 int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n_samples,
@@ -526,9 +965,9 @@ int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n
   if (!samples || !h || !out || n_units > 0x7fffffff) return DRCVAR_ERR_INVALID_ARGUMENT;
   Launch L{samples, n_units, 1, n_samples, stride_unit, 0, stride_sample,
            h, h_stride_unit, 0,
-           Params{robot_radius + obstacle_radius, alpha, delta, epsilon}, out,
+           make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
            static_cast<hipStream_t>(stream)};
-  return dispatch<true>(L);
+  return dispatch<true>(L, 0, 0);
 }
 
 }  // extern "C"

@@ -78,12 +78,27 @@ def _check_pairs(t: torch.Tensor, name: str, rows: int, device: torch.device) ->
                          f"{tuple(t.shape)}")
 
 
+def _typed(args):
+    """Pre-convert an argument tuple to ctypes objects (saves the per-call conversion)."""
+    out = []
+    for a in args:
+        if isinstance(a, ctypes._SimpleCData):
+            out.append(a)
+        elif isinstance(a, bool) or not isinstance(a, (int, float)):
+            raise TypeError(f"unexpected argument {a!r}")
+        elif isinstance(a, int):
+            out.append(ctypes.c_int64(a))
+        else:
+            out.append(ctypes.c_double(a))
+    return tuple(out)
+
+
 class PreparedLaunch:
     """A frozen engine call: same buffers, same parameters, relaunched by ``__call__``."""
 
     def __init__(self, fn, args, keepalive):
         self._fn = fn
-        self._args = args
+        self._args = _typed(args)
         self._keepalive = keepalive  # tensors whose storage the pointers refer to
 
     def __call__(self) -> None:
@@ -93,7 +108,10 @@ class PreparedLaunch:
 
 
 def prepare_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams,
-                            out: torch.Tensor | None = None, stream=None) -> tuple[PreparedLaunch, torch.Tensor]:
+                            out: torch.Tensor | None = None, stream=None,
+                            geometry: tuple[int, int] | None = None) -> tuple[PreparedLaunch, torch.Tensor]:
+    """Freeze one ``drcvar_safe_halfspaces_f64`` call; ``geometry=(threads, per_thread)`` selects a
+    specific compiled launch geometry through ``drcvar_safe_halfspaces_f64_ex`` (tuning)."""
     params.validate()
     _check_samples(samples, 4)
     O, T, N, _ = samples.shape
@@ -109,6 +127,9 @@ def prepare_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: Ri
             ctypes.c_void_p(ego.data_ptr()), ego.stride(0),
             params.robot_radius, params.obstacle_radius, params.alpha, params.delta, params.epsilon,
             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(_stream_handle(samples.device, stream)))
+    if geometry is not None:
+        geo = tuple(ctypes.c_int32(int(g)) for g in geometry)
+        return PreparedLaunch(lib.drcvar_safe_halfspaces_f64_ex, args + geo, (samples, ego, out)), out
     return PreparedLaunch(lib.drcvar_safe_halfspaces_f64, args, (samples, ego, out)), out
 
 

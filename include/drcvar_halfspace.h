@@ -86,6 +86,19 @@ int drcvar_safe_halfspaces_f64(const double* samples, int64_t n_obstacles, int64
                                double* out, void* stream);
 
 /*
+ * drcvar_safe_halfspaces_f64 with an explicit launch geometry (threads per unit and samples held
+ * per thread; both 0 = automatic, the plan drcvar_launch_plan reports).  For tuning: returns
+ * DRCVAR_ERR_UNSUPPORTED when no compiled geometry matches or threads * samples < n_samples.
+ */
+int drcvar_safe_halfspaces_f64_ex(const double* samples, int64_t n_obstacles, int64_t n_steps,
+                                  int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
+                                  int64_t stride_sample, const double* ego_ref_pos,
+                                  int64_t ego_stride_step, double robot_radius,
+                                  double obstacle_radius, double alpha, double delta,
+                                  double epsilon, double* out, void* stream,
+                                  int32_t threads_per_unit, int32_t samples_per_thread);
+
+/*
  * cvar_halfspace / dr_cvar_halfspace for n_units units with a caller-supplied direction
  * h[u] = (h[u*h_stride_unit], h[u*h_stride_unit + 1]) (not necessarily unit length; the combined
  * radius is scaled by |h| exactly as risk_metrics.py:293 / :234 do).  The output record has the

@@ -84,7 +84,8 @@ def offsets_given_h(samples, h, alpha, delta, epsilon, robot_radius, obstacle_ra
     d = h[..., None, 0] * samples[..., 0] + h[..., None, 1] * samples[..., 1]
     finite = np.isfinite(samples).all(axis=(-1, -2))
     L = lower_tail_mean(np.where(finite[..., None], d, 0.0), alpha)
-    ok = finite & (alpha <= 1.0)
+    n = samples.shape[-2]
+    ok = finite & (alpha * n <= n)                              # k = alpha N <= N, else unbounded
     g_cvar = np.where(ok, r - delta - L, SENTINEL)
     ok_dr = ok & (epsilon >= 0.0)
     g_star = np.where(ok_dr, r - delta + epsilon / alpha - L, SENTINEL)

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase shader-clock shares from a -DDRCVAR_STAMPS build (DRCVAR_DIAG_LIB)."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native, engine, synthetic  # noqa: E402
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.engine import RiskParams  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--shape", default="10,20,1000")
+ap.add_argument("--geometry", default="")
+args = ap.parse_args()
+O, T, N = (int(v) for v in args.shape.split(","))
+geo = tuple(int(v) for v in args.geometry.split(",")) if args.geometry else None
+dev = torch.device("cuda", 0)
+s, e = synthetic.obstacle_batch(O, T, N, dev)
+launch, out = engine.prepare_safe_halfspaces(s, e, RiskParams(), geometry=geo)
+for _ in range(30):
+    launch()
+torch.cuda.synchronize()
+lib = _native.lib()
+U = min(O * T, 16384)
+buf = (ctypes.c_ulonglong * (U * 8))()
+lib.drcvar_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+assert lib.drcvar_diag_stamps(ctypes.cast(buf, ctypes.c_void_p), U) == U
+st = np.frombuffer(buf, dtype=np.uint64).reshape(U, 8).astype(np.int64)
+names = ["entry->loads done", "moments reduce+barrier1", "h/var/histogram atomics",
+         "barrier2+scan", "compaction", "barrier3", "rank+finish"]
+d = np.diff(st, axis=1)
+tot = st[:, 7] - st[:, 0]
+print(f"shape {args.shape} geometry {geo}: median unit cycles {np.median(tot):.0f} "
+      f"(min {tot.min()}, max {tot.max()})")
+for k, nm in enumerate(names):
+    print(f"  {nm:28s} median {np.median(d[:, k]):8.0f} cycles  ({np.median(d[:, k]) / np.median(tot) * 100:5.1f}%)")
+span = st[:, 7].max() - st[:, 0].min()
+print(f"  first entry -> last exit span {span} cycles")

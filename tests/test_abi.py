@@ -47,8 +47,8 @@ def test_abi_version_and_strerror():
 
 
 @pytest.mark.parametrize("n,expect", [(1, (64, 2, 128)), (100, (64, 2, 128)), (129, (128, 4, 256)),
-                                      (1000, (256, 4, 512)), (5000, (512, 16, 4096)),
-                                      (10000, (1024, 10, 4096)), (16384, (1024, 16, 4096))])
+                                      (1000, (256, 4, 512)), (5000, (512, 16, 1024)),
+                                      (10000, (512, 20, 1024)), (16384, (1024, 16, 1024))])
 def test_launch_plan(n, expect):
     b, p, nb = _native.launch_plan(n)
     assert (b, p, nb) == expect

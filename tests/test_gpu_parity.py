@@ -195,3 +195,26 @@ def test_config5_full_size_properties():
     _assert_match(r[::37, ::7], want)
     del s, rec, rec2
     torch.cuda.empty_cache()
+
+
+GEOMETRIES = [(64, 2), (128, 4), (256, 4), (256, 8), (256, 16), (512, 16), (512, 20), (1024, 12),
+              (1024, 16), (64, 16), (128, 8), (512, 2), (1024, 10), (256, 20)]
+
+
+@pytest.mark.parametrize("n", [100, 1000, 5000, 10000])
+def test_every_geometry_agrees(n):
+    """All compiled launch geometries (drcvar_safe_halfspaces_f64_ex) give the oracle's answer."""
+    rng = np.random.default_rng(n + 1)
+    samples = rng.normal(size=(2, 3, n, 2)) * 0.2 + rng.uniform(-3, 3, size=(2, 3, 1, 2))
+    samples[0, 0] = np.round(samples[0, 0], 1)   # heavy ties -> refinement path
+    samples[1, 0] = 1.5                          # zero variance -> degenerate path
+    ego = rng.uniform(-3, 3, size=(3, 2))
+    want = c_oracle.safe_halfspaces(samples, ego, 0.3, 0.3, 0.2, 0.1, 0.15)
+    s = torch.as_tensor(samples).to(DEV)
+    e = torch.as_tensor(ego).to(DEV)
+    for g in GEOMETRIES:
+        if g[0] * g[1] < n:
+            continue
+        launch, out = engine.prepare_safe_halfspaces(s, e, RiskParams(), geometry=g)
+        launch()
+        _assert_match(out.cpu().numpy(), want)
