@@ -6,15 +6,23 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one evaluation of the hot path over one batch: every (obstacle, horizon-step) unit of a
-synthetic [O, T, N, 2] fp64 sample tensor -> mean / CVaR / DR-CVaR halfspaces (one fused kernel
-launch).  Default workload c3 = BASELINE.json's metric config (10 obstacles, T = 20, N = 1000).
-Inputs are generated on the device and resident in HBM before timing starts.  Multi-GPU: one
-process per GPU, every rank evaluates its own batch (weak scaling, no data-path collective); with
---gather each step also all-gathers the [U, 8] records over RCCL (the QP hand-off exchange).
+synthetic [O, T, N, 2] fp64 sample tensor -> mean / CVaR / DR-CVaR halfspaces, i.e. ONE launch
+of the fused kernel through the C ABI.  Default workload c3 = BASELINE.json's metric config
+(10 obstacles, T = 20, N = 1000).  Inputs are generated on the device and resident in HBM before
+timing starts.  A c3 launch is ~6 us, so by default the K steps are issued as replays of a
+hipGraph that holds `--graph-batch` consecutive launches (every replayed launch recomputes the
+whole batch; `--launch eager` issues one ctypes call per step instead).
 
-Prints ONE JSON line on rank 0 (contract in the task statement): value = units of all ranks / max
-rank time, plus `roofline` (dominant kernel, HIP events on its stream), `cpu_baseline` (the C
-oracle, 1 thread, on a bounded sample of the same batch) and `max_abs_err` vs that oracle.
+Multi-GPU: one process per GPU; every rank evaluates its own batch (weak scaling, no data-path
+collective); with --gather each step also all-gathers the [U, 8] records over RCCL (the QP
+hand-off exchange).
+
+Prints ONE JSON line on rank 0: value = units of all ranks / max rank time, plus
+  roofline        the kernel on this workload: algorithmic bytes per launch / (HIP-event time over
+                  the timed region / K) — includes the ~1 us inter-launch gap, so a lower bound
+  roofline_large  the same kernel on a 2 GB resident batch (256 x 50 x 10 000), event-timed
+  cpu_baseline    oracle/drcvar_oracle.c (1 thread) on whole batches of the same workload
+  max_abs_err     max |offset - oracle| over the benchmarked batch (the metric's second half)
 """
 from __future__ import annotations
 
@@ -40,12 +48,13 @@ WORKLOADS = {
     "c4": (64, 30, 5000, "synthetic 64 obstacles, T=30, N=5000 (BASELINE config 4, per GPU)"),
     "c5": (256, 50, 10000, "synthetic 256 obstacles, T=50, N=10000 (BASELINE config 5, per GPU)"),
 }
+LARGE = (256, 50, 10000)
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 OUT_BYTES = 64     # 8 fp64 per unit
 
 
 def algorithmic_bytes(O, T, N):
-    """Bytes one launch must move: samples once (16 B each), the 64-B record, ego per step."""
+    """Bytes one launch must move: every sample once (16 B), the 64-B record, ego per step."""
     return O * T * (16 * N + OUT_BYTES) + T * 16
 
 
@@ -57,6 +66,13 @@ def load_traffic(workload):
             return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def roofline(abytes, kernel_s, traffic):
+    achieved = abytes / kernel_s
+    return {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel_ms": kernel_s * 1e3,
+            "algorithmic_bytes_per_launch": abytes}
 
 
 def cpu_baseline(samples, ego, params, budget_s):
@@ -80,16 +96,50 @@ def cpu_baseline(samples, ego, params, budget_s):
                            f"({el:.1f} s, oracle/drcvar_oracle.c quickselect, 1 thread)"}
 
 
+class Stepper:
+    """Issues steps: eager ctypes launches, or replays of a hipGraph holding G launches."""
+
+    def __init__(self, samples, ego, params, mode, graph_batch, dev):
+        self.mode = mode
+        self.G = graph_batch if mode == "graph" else 1
+        self.launch, self.out = engine.prepare_safe_halfspaces(samples, ego, params)
+        if mode == "graph":
+            self.launch()  # warm the code object before capture
+            torch.cuda.synchronize(dev)
+            self.graph = torch.cuda.CUDAGraph()
+            cap_stream = torch.cuda.Stream(dev)
+            with torch.cuda.graph(self.graph, stream=cap_stream):
+                # the frozen call must target the capturing stream
+                cap, _ = engine.prepare_safe_halfspaces(samples, ego, params, out=self.out,
+                                                        stream=torch.cuda.current_stream(dev))
+                for _ in range(self.G):
+                    cap()
+            self._keep = cap
+
+    def run(self, steps):
+        """Issue `steps` steps (rounded up to whole graph replays); returns steps issued."""
+        if self.mode == "graph":
+            reps = -(-steps // self.G)
+            for _ in range(reps):
+                self.graph.replay()
+            return reps * self.G
+        for _ in range(steps):
+            self.launch()
+        return steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--launch", default="graph", choices=["graph", "eager"])
+    ap.add_argument("--graph-batch", type=int, default=50)
     ap.add_argument("--gather", action="store_true", help="all-gather records each step (RCCL)")
-    ap.add_argument("--no-events", action="store_true", help="skip per-step HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-large", action="store_true", help="skip the 2 GB roofline measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,69 +155,71 @@ def main():
     O, T, N, desc = WORKLOADS[args.workload]
     params = RiskParams()  # config/parameters.py: alpha 0.2, delta 0.1, eps 0.15, radii 0.3/0.3
     samples, ego = synthetic.obstacle_batch(O, T, N, dev, seed=42 + rank)
-    stream = torch.cuda.current_stream(dev)
-    launch, out = engine.prepare_safe_halfspaces(samples, ego, params, stream=stream)
     U = O * T
+    mode = "eager" if (args.gather and world > 1) else args.launch  # collectives stay eager
+    stepper = Stepper(samples, ego, params, mode, args.graph_batch, dev)
+    out = stepper.out
     gathered = None
     if args.gather and world > 1:
         gathered = torch.empty((U * world, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
 
-    def step():
-        launch()
-        if gathered is not None:
+    def steps(k):
+        if gathered is None:
+            return stepper.run(k)
+        for _ in range(k):
+            stepper.launch()
             dist.all_gather_into_tensor(gathered, out.view(U, engine.OUT_WIDTH))
+        return k
 
-    for _ in range(args.warmup):
-        step()
+    steps(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    K = args.steps
-    use_events = not args.no_events
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)] if use_events else []
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    if use_events:
-        for k in range(K):
-            ev[k][0].record(stream)
-            launch()
-            ev[k][1].record(stream)
-            if gathered is not None:
-                dist.all_gather_into_tensor(gathered, out.view(U, engine.OUT_WIDTH))
-    else:
-        for _ in range(K):
-            step()
+    ev0.record(stream)
+    K = steps(args.steps)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) * 1e-3 / K
 
-    kernel_ms = None
-    if use_events:
-        durs = [a.elapsed_time(b) for a, b in ev]
-        kernel_ms = sum(durs) / len(durs)
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    k_max = torch.tensor([kernel_ms or 0.0], dtype=torch.float64, device=dev)
+    t_max = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(k_max, op=dist.ReduceOp.MAX)
-    elapsed = float(t_max.item())
+    elapsed, kernel_s = float(t_max[0].item()), float(t_max[1].item())
+
+    large = None
+    if rank == 0 and not args.no_large:
+        Ol, Tl, Nl = LARGE
+        s_l, e_l = synthetic.obstacle_batch(Ol, Tl, Nl, dev, seed=7)
+        launch_l, _ = engine.prepare_safe_halfspaces(s_l, e_l, params)
+        for _ in range(3):
+            launch_l()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        a.record(stream)
+        for _ in range(reps):
+            launch_l()
+        b.record(stream)
+        torch.cuda.synchronize()
+        large = roofline(algorithmic_bytes(Ol, Tl, Nl), a.elapsed_time(b) * 1e-3 / reps,
+                         load_traffic("c5"))
+        large["workload"] = f"{Ol} obstacles x {Tl} steps x {Nl} samples (2.05 GB resident)"
+        large["halfspaces_per_s"] = Ol * Tl / (large["kernel_ms"] * 1e-3)
+        del s_l, e_l
+        torch.cuda.empty_cache()
 
     result = None
     if rank == 0:
         value = U * world * K / elapsed
-        abytes = algorithmic_bytes(O, T, N)
-        roofline = None
-        if use_events:
-            kms = float(k_max.item())
-            achieved = abytes / (kms * 1e-3)
-            traffic = load_traffic(args.workload)
-            roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                        "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                        "kernel_ms": kms, "algorithmic_bytes_per_launch": abytes}
         result = {
             "metric": "halfspace-constraints/sec (N=1000, 10 obs, T=20) + max |offset - ref|",
             "value": value,
@@ -184,15 +236,17 @@ def main():
             "config": {"workload": f"{args.workload}: {desc}", "obstacles": O, "steps": T,
                        "samples": N, "units_per_gpu": U, "global_units_per_step": U * world,
                        "parallelism": f"dp{world}" + ("+allgather" if gathered is not None else ""),
+                       "launch": (f"hipGraph replays of {stepper.G} launches" if mode == "graph"
+                                  else "eager ctypes launch per step"),
                        "alpha": params.alpha, "delta": params.delta, "epsilon": params.epsilon},
-            "roofline": roofline,
+            "roofline": roofline(algorithmic_bytes(O, T, N), kernel_s, load_traffic(args.workload)),
+            "roofline_large": large,
         }
         if world == 1 and not args.no_cpu_baseline:
-            ref, base = cpu_baseline(samples, ego, params, args.cpu_seconds)
             import numpy as np
+            ref, base = cpu_baseline(samples, ego, params, args.cpu_seconds)
             got = out.cpu().numpy()
-            cols = [2, 5, 6, 7]
-            result["max_abs_err"] = float(np.max(np.abs(got[..., cols] - ref[..., cols])))
+            result["max_abs_err"] = float(np.max(np.abs(got[..., [2, 5, 6, 7]] - ref[..., [2, 5, 6, 7]])))
             result["max_abs_err_h"] = float(np.max(np.abs(got[..., [0, 1, 3, 4]] - ref[..., [0, 1, 3, 4]])))
             base["host_cpu"] = _cpu_model()
             base["host_threads_visible"] = os.cpu_count()
