@@ -140,6 +140,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true", help="skip the 2 GB roofline measurement")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path (several ranks may share one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,10 +149,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local_rank >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local_rank} but only {ndev} GPUs visible")
+    dev = torch.device("cuda", local_rank % ndev)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     O, T, N, desc = WORKLOADS[args.workload]
     params = RiskParams()  # config/parameters.py: alpha 0.2, delta 0.1, eps 0.15, radii 0.3/0.3
@@ -161,14 +169,16 @@ def main():
     out = stepper.out
     gathered = None
     if args.gather and world > 1:
-        gathered = torch.empty((U * world, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
+        gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        gathered = torch.empty((U * world, engine.OUT_WIDTH), dtype=torch.float64, device=gdev)
 
     def steps(k):
         if gathered is None:
             return stepper.run(k)
         for _ in range(k):
             stepper.launch()
-            dist.all_gather_into_tensor(gathered, out.view(U, engine.OUT_WIDTH))
+            rec = out.view(U, engine.OUT_WIDTH)
+            dist.all_gather_into_tensor(gathered, rec if gathered.is_cuda else rec.cpu())
         return k
 
     steps(args.warmup)
@@ -190,7 +200,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_s = ev0.elapsed_time(ev1) * 1e-3 / K
 
-    t_max = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=dev)
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    t_max = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed, kernel_s = float(t_max[0].item()), float(t_max[1].item())

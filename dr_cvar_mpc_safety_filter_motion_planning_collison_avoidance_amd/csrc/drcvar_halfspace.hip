@@ -70,6 +70,7 @@ struct Params {
   double inv_k;           // 1 / (alpha N)
   double z_alpha;         // standard-normal alpha-quantile: centre of the fast-path window
   double window_sd;       // half-width of the fast-path window, in sd of d
+  double hist_scale;      // bins / (2 window_sd): bins per sd of d (set per launch plan)
   uint32_t rank;          // min(floor(alpha N), N - 1): 0-based rank of tau
   int unbounded;          // alpha N > N: both LPs unbounded (tau -> -inf), solver-failure sentinel
   double degenerate_sq;   // smallest x with sqrt(x) >= 1e-10: |v| < 1e-10  <=>  v.v < degenerate_sq
@@ -199,9 +200,10 @@ struct ScanResult {
 // Histogram storage: lane l of a scanning wave owns bins [l*B, (l+1)*B), B = NB/64.  One padding
 // word after every B bins makes the owner reads conflict-free (lane stride B+1 words, B+1 odd).
 template <int NB>
-__device__ __forceinline__ int hist_slot(int bin) {
-  constexpr int B = NB / kWave;
-  return bin + bin / B;
+__device__ __forceinline__ int hist_slot(int bin) {  // bin >= 0
+  constexpr unsigned B = NB / kWave;
+  const unsigned b = static_cast<unsigned>(bin);
+  return static_cast<int>(b + b / B);
 }
 template <int NB>
 constexpr int hist_words() {
@@ -550,6 +552,15 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       y[j] = base[off + 1];
     }
   }
+  // The unit's direction input and the early scalars are fetched while the 16-B sample loads
+  // are in flight (otherwise the compiler sinks these scalar loads to their first use, after
+  // barrier 1, and their latency lands on the critical path).
+  const double* dp = dir + o * dir_s_obs + t * dir_s_step;
+  const double e0 = dp[0], e1 = dp[1];
+  const double inv_n = prm.inv_n, inv_n0 = prm.inv_n0, deg_sq = prm.degenerate_sq;
+  const double z_alpha = prm.z_alpha, window_sd = prm.window_sd, hist_scale = prm.hist_scale;
+  asm volatile("" ::"s"(e0), "s"(e1), "s"(inv_n), "s"(inv_n0), "s"(deg_sq), "s"(z_alpha),
+               "s"(window_sd), "s"(hist_scale));
   // Sums for the mean over every sample (plain sums, as np.mean); second moments over row 0 only
   // (the first BLOCK samples) — they merely position the fast-path window, so a subsample is
   // enough and cancellation in them can only cost speed, never exactness.
@@ -571,7 +582,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   DRCVAR_STAMP(1);
   block_reduce<OpAdd, NW, 7>(mom, red_mom);                              // [barrier 1]
   DRCVAR_STAMP(2);
-  const double mux = mom[0] * prm.inv_n, muy = mom[1] * prm.inv_n;
+  const double mux = mom[0] * inv_n, muy = mom[1] * inv_n;
   // any non-finite sample makes a sum non-finite (so do sums that overflow): solver failure
   const bool bad = !(std::isfinite(mom[0]) && std::isfinite(mom[1]));
 #if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 1
@@ -580,16 +591,15 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 #endif
 
   // ---- 2. direction ----------------------------------------------------------------------
-  const double* dp = dir + o * dir_s_obs + t * dir_s_step;
   double h0, h1;
   if constexpr (GIVEN_H) {
-    h0 = dp[0];
-    h1 = dp[1];
+    h0 = e0;
+    h1 = e1;
   } else {  // compute_separating_vector(ego, mu), core/geometry.py:35-53
-    const double dx = mux - dp[0], dy = muy - dp[1];
+    const double dx = mux - e0, dy = muy - e1;
     const double n2 = dx * dx + dy * dy;
     const double inv = std::isfinite(n2) ? rsqrt_nr(n2) : 1.0 / sqrt(n2);  // inf: as diff/norm
-    const bool degenerate = n2 < prm.degenerate_sq;  // |mu - ego| < 1e-10 -> [1, 0]
+    const bool degenerate = n2 < deg_sq;  // |mu - ego| < 1e-10 -> [1, 0]
     h0 = degenerate ? 1.0 : dx * inv;
     h1 = degenerate ? 0.0 : dy * inv;
   }
@@ -609,18 +619,18 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   for (int j = 0; j < P; ++j)  // +inf padding: never below, inside or a candidate
     d[j] = (tid + j * BLOCK < n) ? project(h0, h1, x[j], y[j]) : INFINITY;
   const double mu_d = h0 * mux + h1 * muy;
-  const double ma0 = mom[2] * prm.inv_n0, mb0 = mom[3] * prm.inv_n0;  // row-0 covariance
-  const double cxx = mom[4] * prm.inv_n0 - ma0 * ma0, cyy = mom[5] * prm.inv_n0 - mb0 * mb0;
-  const double cxy = mom[6] * prm.inv_n0 - ma0 * mb0;
+  const double ma0 = mom[2] * inv_n0, mb0 = mom[3] * inv_n0;  // row-0 covariance
+  const double cxx = mom[4] * inv_n0 - ma0 * ma0, cyy = mom[5] * inv_n0 - mb0 * mb0;
+  const double cxy = mom[6] * inv_n0 - ma0 * mb0;
   const double var_d = h0 * h0 * cxx + 2.0 * h0 * h1 * cxy + h1 * h1 * cyy;
   // window [wlo, whi] = mean_d + (z_alpha -+ window_sd) sd_d; only samples inside it are
   // histogrammed (LDS atomics), samples below it are counted with ballots.  Any positive scale
   // keeps the map monotone, so the approximate reciprocal square root is exact enough.
   const double inv_sd = rsqrt_nr(var_d);
   const double sd_d = var_d * inv_sd;
-  const double wlo = mu_d + (prm.z_alpha - prm.window_sd) * sd_d;
-  const double whi = mu_d + (prm.z_alpha + prm.window_sd) * sd_d;
-  const LinearMap<NB> map{wlo, static_cast<double>(NB) / (2.0 * prm.window_sd) * inv_sd};
+  const double wlo = mu_d + (z_alpha - window_sd) * sd_d;
+  const double whi = mu_d + (z_alpha + window_sd) * sd_d;
+  const LinearMap<NB> map{wlo, prm.hist_scale * inv_sd};
   const uint32_t rank = prm.rank;
   bool fast = var_d > 0.0 && std::isfinite(map.scale) && std::isfinite(wlo) && map.scale > 0.0;
   uint32_t rr = rank, c = 0;
@@ -780,6 +790,7 @@ template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
 void launch_plan(Launch L, bool vec) {
   const dim3 grid(static_cast<unsigned>(L.units)), block(BLOCK);
   L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < BLOCK ? L.n : BLOCK);
+  L.prm.hist_scale = static_cast<double>(1 << LOG_NB) / (2.0 * L.prm.window_sd);
   if (vec) {
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, true, GIVEN_H>), grid, block, 0,
                        L.stream, L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
