@@ -17,9 +17,10 @@ LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libdrcvar_halfspace.so")
 # diagnostic builds only (scripts/diag_stages.sh); the product always loads LIB_PATH
 LIB_PATH = os.environ.get("DRCVAR_DIAG_LIB", LIB_PATH)
-SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip")]
+SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip"),
+           os.path.join(PKG_DIR, "csrc", "drcvar_mpc.hip")]
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
-HEADER = os.path.join(INCLUDE_DIR, "drcvar_halfspace.h")
+HEADERS = [os.path.join(INCLUDE_DIR, "drcvar_halfspace.h"), os.path.join(INCLUDE_DIR, "drcvar_mpc.h")]
 OFFLOAD_ARCH = os.environ.get("DRCVAR_OFFLOAD_ARCH", "gfx950")
 
 ABI_VERSION = 1
@@ -30,7 +31,27 @@ COL_MEAN_H0, COL_MEAN_H1, COL_G_MEAN, COL_H0, COL_H1, COL_G_CVAR, COL_G_DR_STAR,
 # return codes (include/drcvar_halfspace.h)
 OK, ERR_INVALID_ARGUMENT, ERR_UNSUPPORTED, ERR_LAUNCH = 0, 1, 2, 3
 
-# Every symbol include/drcvar_halfspace.h declares (checked by tests/test_abi.py).
+# MPC hand-off (include/drcvar_mpc.h)
+MPC_MAX_STATES, MPC_MAX_INPUTS, MPC_MAX_HORIZON, MPC_MAX_DECISION = 8, 4, 64, 120
+MPC_INFO_WIDTH = 10
+(MPC_INFO_STATUS, MPC_INFO_ITERATIONS, MPC_INFO_OBJECTIVE, MPC_INFO_MU, MPC_INFO_PRIMAL_RES,
+ MPC_INFO_DUAL_RES, MPC_INFO_MAX_SLACK, MPC_INFO_USED_FALLBACK, MPC_INFO_POLISHED,
+ MPC_INFO_POLISH_ATTEMPTS) = range(10)
+MPC_STATUS_OPTIMAL, MPC_STATUS_MAX_ITER, MPC_STATUS_NUMERICAL, MPC_STATUS_OPTIMAL_INACCURATE = 0, 1, 2, 3
+
+
+class MpcModel(ctypes.Structure):
+    """``drcvar_mpc_model`` (include/drcvar_mpc.h)."""
+
+    _fields_ = [("n_states", ctypes.c_int32), ("n_inputs", ctypes.c_int32),
+                ("n_outputs", ctypes.c_int32), ("horizon", ctypes.c_int32),
+                ("has_input_bounds", ctypes.c_int32), ("has_position_bounds", ctypes.c_int32),
+                ("u_min", ctypes.c_double * MPC_MAX_INPUTS), ("u_max", ctypes.c_double * MPC_MAX_INPUTS),
+                ("p_min", ctypes.c_double * 2), ("p_max", ctypes.c_double * 2),
+                ("blob_doubles", ctypes.c_int64)]
+
+
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "drcvar_abi_version",
     "drcvar_strerror",
@@ -38,6 +59,9 @@ EXPORTED_SYMBOLS = (
     "drcvar_safe_halfspaces_f64_ex",
     "drcvar_offsets_given_h_f64",
     "drcvar_launch_plan",
+    "drcvar_mpc_model_init",
+    "drcvar_mpc_workspace_doubles",
+    "drcvar_mpc_filter_f64",
 )
 
 
@@ -87,6 +111,16 @@ def _bind(lib):
     lib.drcvar_offsets_given_h_f64.restype = ctypes.c_int
     lib.drcvar_launch_plan.argtypes = [i64, i32p, i32p, i32p]
     lib.drcvar_launch_plan.restype = ctypes.c_int
+    i32, modelp = ctypes.c_int32, ctypes.POINTER(MpcModel)
+    lib.drcvar_mpc_model_init.argtypes = [ptr, ptr, ptr, ptr, ptr, i32, i32, i32, i32,
+                                          ptr, ptr, ptr, ptr, modelp, ptr]
+    lib.drcvar_mpc_model_init.restype = ctypes.c_int
+    lib.drcvar_mpc_workspace_doubles.argtypes = [modelp, i64, i64]
+    lib.drcvar_mpc_workspace_doubles.restype = i64
+    lib.drcvar_mpc_filter_f64.argtypes = [
+        modelp, ptr, i64, ptr, ptr, i64, i64, i64, i64, i64, i64, i64, i64, ptr, i64, ptr, i64,
+        i64, ptr, i64, i64, i32, dbl, i32, ptr, ptr, ptr, ptr, i64, ptr]
+    lib.drcvar_mpc_filter_f64.restype = ctypes.c_int
     return lib
 
 

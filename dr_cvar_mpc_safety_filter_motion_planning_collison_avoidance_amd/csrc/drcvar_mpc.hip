@@ -1,0 +1,1393 @@
+// drcvar_mpc.hip — the MPC safety-filter QP that consumes the safe halfspaces, for gfx950.
+//
+// Reference: core/mpc_filter.py:40-178 (MPCSafetyFilter.filter_trajectory) builds, per call, a
+// CVXPY problem over x [H+1, nx], u [H, nu] and one slack per halfspace, solves it with the default
+// QP solver and falls back to a rolled-out input sequence (_fallback, :180-219) when the solve does
+// not succeed.  Here every problem of a batch is one workgroup that runs a primal-dual Mehrotra
+// interior-point method to convergence without leaving the device.
+//
+// Formulation (input space; the dynamics are eliminated once on the host, drcvar_mpc_model_init):
+//   positions  p_{k+1} = c_k + sum_{j<=k} Mp[k-j] u_j,  Mp[i] = C A^i B,  c_k = C A^{k+1} x0
+//   objective  1/2 u'H0 u + f'u + sum_r 50 s_r + 50 s_r^2,  H0 = 2(Gx'QGx + R), f = F1 x0 - F2 xr
+//   rows       halfspace r (step k):   h.p_{k+1} + g - s_r <= 0      (w_hs, lambda_hs)
+//              slack sign:             -s_r <= 0                      (w_s,  lambda_s)
+//              input box (optional):   u_j - u_max <= 0, u_min - u_j <= 0
+//              position box (optional): p - p_max <= 0, p_min - p <= 0 (per step and coordinate)
+// Newton system: the slack columns are diagonal and are eliminated per row, so the halfspaces of
+// step k reach the input-space Hessian only through the 2x2 matrix S_k = sum_r omega_r h_r h_r'
+// and the right-hand side through a 2-vector per step:
+//   K = H0 + diag(D_box) + sum_k Mp_k' S_k Mp_k    (n x n, n = nu*H <= 120, Cholesky in LDS)
+// so the per-iteration cost is O(rows) streaming + O(n^3) dense work independent of the number of
+// obstacles.  Rows live in a per-problem workspace ([O, 64] SoA arrays, lane = halfspace step, so
+// every row pass is a coalesced sweep); per-step sums are combined across waves in a fixed order,
+// so the solver is deterministic.
+//
+// Iteration (Mehrotra predictor-corrector, identical to oracle-independent prototype
+// scripts/mpc_condensed_proto.py):
+//   P1 residuals, weights, per-step S / v / affine z          -> r_du, convergence test
+//   assemble K, Cholesky; affine direction (solve); P2 affine step length
+//   P3 affine gap + corrector rhs split as base + sigma*mu*unit; corrector direction (solve)
+//   P4 corrector step length; P5 update (step 0.995 of the way to the boundary)
+// Affine directions of a row are recomputed from (state, dp_aff) instead of being stored.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "drcvar_mpc.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
+constexpr int kRowArrays = 8; // h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
+constexpr int kBestPad = 128; // best iterate u (n <= DRCVAR_MPC_MAX_DECISION)
+constexpr double kSlackLin = 50.0;    // core/mpc_filter.py:143
+constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:144
+constexpr double kStepFrac = 0.995;
+constexpr double kHuge = 1e300;
+constexpr int kPerStepQ = 7;          // per-step partial sums carried by one reduction
+constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
+constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
+constexpr int kPolishAttempts = 4;    // active-set corrections
+constexpr double kPolishMerit = 1e-6; // polish only from an iterate this close to the optimum
+constexpr double kPolishDualTol = 1e-7;
+
+struct BlobLayout {
+  int64_t H0, F1, F2, Mp, CA, A, B, Q, R, total;
+};
+
+BlobLayout blob_layout(int nx, int nu, int H) {
+  const int64_t n = static_cast<int64_t>(nu) * H;
+  BlobLayout L{};
+  int64_t o = 0;
+  L.H0 = o; o += n * n;
+  L.F1 = o; o += n * nx;
+  L.F2 = o; o += n * H * nx;
+  L.Mp = o; o += static_cast<int64_t>(H) * 2 * nu;
+  L.CA = o; o += static_cast<int64_t>(H) * 2 * nx;
+  L.A = o; o += nx * nx;
+  L.B = o; o += nx * nu;
+  L.Q = o; o += nx * nx;
+  L.R = o; o += nu * nu;
+  L.total = o;
+  return L;
+}
+
+struct MpcArgs {
+  const double* blob;
+  BlobLayout off;
+  int nx, nu, H, n, K, O, ld;
+  int has_u, has_p;
+  double umin[DRCVAR_MPC_MAX_INPUTS], umax[DRCVAR_MPC_MAX_INPUTS], pmin[2], pmax[2];
+  const double* hs_h;
+  const double* hs_g;
+  int64_t h_sp, h_so, h_sk, g_sp, g_so, g_sk;
+  const double* x0;
+  int64_t x0_sp;
+  const double* xr;
+  int64_t xr_sp, xr_st;
+  const double* uf;
+  int64_t uf_sp, uf_st;
+  double* x_out;
+  double* u_out;
+  double* info;
+  double* ws;
+  int64_t ws_pp;
+  int max_iter;
+  double tol;
+  int polish;
+};
+
+// LDS carve (doubles), sized from (n, H, ld) only; lds_doubles() and carve() must agree.
+struct Lds {
+  double* K;      // [n][ld] lower triangle, overwritten by the Cholesky factor
+  double* diag;   // [n] pivots L_jj
+  double* u;      // [n] inputs (the iterate)
+  double* dua;    // [n] affine direction
+  double* du;     // [n] corrector direction
+  double* rdu;    // [n] dual residual of the inputs
+  double* f;      // [n] linear cost
+  double* DU;     // [n] box weights
+  double* rU;     // [n] box rhs term (affine, then corrector base)
+  double* rUu;    // [n] box rhs term (corrector unit)
+  double* bx;     // [4][n] box state wUu, lUu, wUl, lUl
+  double* c;      // [2H] free-response positions
+  double* p;      // [2H] positions of the iterate
+  double* dpa;    // [2H] affine position direction
+  double* dp;     // [2H] corrector position direction
+  double* v;      // [2H] per-step sum of lambda_hs h (+ position-box duals)
+  double* za;     // [2H] per-step affine rhs, then corrector base
+  double* zu;     // [2H] per-step corrector unit
+  double* px;     // [4][2H] position-box state wPu, lPu, wPl, lPl
+  double* S;      // [3][H] per-step 2x2 weights (S00, S01, S11)
+  double* Mp;     // [H][2][NU] C A^i B
+  double* xs;     // [H+1][nx] rollout
+  double* red;    // [kWaves][kPerStepQ][64] per-step partial sums
+  double* sc;     // [64] block scalars
+};
+
+inline int64_t lds_doubles(int n, int H, int ld) {
+  return static_cast<int64_t>(n) * ld + 13LL * n + 14LL * H + 8LL * H + 3LL * H +
+         2LL * DRCVAR_MPC_MAX_INPUTS * H + static_cast<int64_t>(H + 1) * DRCVAR_MPC_MAX_STATES +
+         static_cast<int64_t>(kWaves) * kPerStepQ * 64 + 64;
+}
+
+__device__ inline Lds carve(double* base, int n, int H, int ld) {
+  Lds s;
+  double* q = base;
+  s.K = q; q += static_cast<int64_t>(n) * ld;
+  s.diag = q; q += n;
+  s.u = q; q += n;
+  s.dua = q; q += n;
+  s.du = q; q += n;
+  s.rdu = q; q += n;
+  s.f = q; q += n;
+  s.DU = q; q += n;
+  s.rU = q; q += n;
+  s.rUu = q; q += n;
+  s.bx = q; q += 4 * n;
+  s.c = q; q += 2 * H;
+  s.p = q; q += 2 * H;
+  s.dpa = q; q += 2 * H;
+  s.dp = q; q += 2 * H;
+  s.v = q; q += 2 * H;
+  s.za = q; q += 2 * H;
+  s.zu = q; q += 2 * H;
+  s.px = q; q += 8 * H;
+  s.S = q; q += 3 * H;
+  s.Mp = q; q += 2 * DRCVAR_MPC_MAX_INPUTS * H;
+  s.xs = q; q += (H + 1) * DRCVAR_MPC_MAX_STATES;
+  s.red = q; q += kWaves * kPerStepQ * 64;
+  s.sc = q;
+  return s;
+}
+
+// ---- reductions (butterflies: every lane ends with the bitwise-identical value) ----
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m));
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m));
+  return v;
+}
+
+// Three block-wide reductions (sum, max, max) in one LDS round trip; waves combined in order.
+__device__ inline void block_sum_max_max(double& a, double& b, double& c, double* sc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_sum(a);
+  b = wave_max(b);
+  c = wave_max(c);
+  if (lane == 0) {
+    sc[wave] = a;
+    sc[kWaves + wave] = b;
+    sc[2 * kWaves + wave] = c;
+  }
+  __syncthreads();
+  a = sc[0];
+  b = sc[kWaves];
+  c = sc[2 * kWaves];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) {
+    a += sc[w];
+    b = fmax(b, sc[kWaves + w]);
+    c = fmax(c, sc[2 * kWaves + w]);
+  }
+  __syncthreads();
+}
+
+__device__ inline double block_min(double a, double* sc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_min(a);
+  if (lane == 0) sc[3 * kWaves + wave] = a;
+  __syncthreads();
+  double r = sc[3 * kWaves];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) r = fmin(r, sc[3 * kWaves + w]);
+  __syncthreads();
+  return r;
+}
+
+__device__ inline double block_sum(double a, double* sc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_sum(a);
+  if (lane == 0) sc[4 * kWaves + wave] = a;
+  __syncthreads();
+  double r = sc[4 * kWaves];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) r += sc[4 * kWaves + w];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double ratio(double x, double dx) { return dx < 0.0 ? -x / dx : kHuge; }
+
+// p[2k+i] = c[2k+i] + sum_{j<=k} Mp[k-j][i][:] . u[j*nu : (j+1)*nu]
+template <int NU>
+__device__ inline void positions(const Lds& s, const double* u, double* out, const double* c, int H) {
+  for (int t = threadIdx.x; t < 2 * H; t += kBlock) {
+    const int k = t >> 1, i = t & 1;
+    double acc = c ? c[t] : 0.0;
+    for (int j = 0; j <= k; ++j) {
+      const double* m = s.Mp + ((k - j) * 2 + i) * NU;
+#pragma unroll
+      for (int a = 0; a < NU; ++a) acc += m[a] * u[j * NU + a];
+    }
+    out[t] = acc;
+  }
+}
+
+// out[j*nu+a] (+)= sum_{k>=j} sum_i Mp[k-j][i][a] z[2k+i]
+template <int NU>
+__device__ inline double gp_transpose(const Lds& s, const double* z, int j_a, int H) {
+  const int j = j_a / NU, a = j_a - j * NU;
+  double acc = 0.0;
+  for (int k = j; k < H; ++k) {
+    const double* m = s.Mp + (k - j) * 2 * NU;
+    acc += m[a] * z[2 * k] + m[NU + a] * z[2 * k + 1];
+  }
+  return acc;
+}
+
+// K = H0 + diag(DU) + sum_k Mp_k' S_k Mp_k, lower nu x nu blocks (jb >= lb), one block per thread.
+template <int NU>
+__device__ inline void assemble_hessian(const Lds& s, const double* H0, int n, int ld, int H) {
+  for (int blk = threadIdx.x; blk < H * H; blk += kBlock) {
+    const int jb = blk / H, lb = blk - jb * H;
+    if (lb > jb) continue;
+    double acc[NU][NU];
+#pragma unroll
+    for (int x = 0; x < NU; ++x)
+#pragma unroll
+      for (int y = 0; y < NU; ++y) acc[x][y] = 0.0;
+    for (int k = jb; k < H; ++k) {
+      const double S00 = s.S[k], S01 = s.S[H + k], S11 = s.S[2 * H + k];
+      const double* Mj = s.Mp + (k - jb) * 2 * NU;
+      const double* Ml = s.Mp + (k - lb) * 2 * NU;
+#pragma unroll
+      for (int y = 0; y < NU; ++y) {
+        const double t0 = S00 * Ml[y] + S01 * Ml[NU + y];
+        const double t1 = S01 * Ml[y] + S11 * Ml[NU + y];
+#pragma unroll
+        for (int x = 0; x < NU; ++x) acc[x][y] += Mj[x] * t0 + Mj[NU + x] * t1;
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < NU; ++x) {
+      const int row = jb * NU + x;
+#pragma unroll
+      for (int y = 0; y < NU; ++y) {
+        const int col = lb * NU + y;
+        double val = H0[static_cast<int64_t>(row) * n + col] + acc[x][y];
+        if (row == col) val += s.DU[row];
+        s.K[row * ld + col] = val;
+      }
+    }
+  }
+}
+
+// Right-looking Cholesky of the lower triangle of K (n x n, leading dimension ld), in place;
+// s.diag[j] = L_jj.  Two barriers per column.  Returns false on a non-positive/non-finite pivot.
+__device__ inline bool cholesky(const Lds& s, int n, int ld) {
+  const int tid = threadIdx.x;
+  double* K = s.K;
+  for (int j = 0; j < n; ++j) {
+    const double d = K[j * ld + j];
+    if (!(d > 0.0) || !isfinite(d)) return false;  // uniform: every thread read the same value
+    const double rs = sqrt(d);
+    const double inv = 1.0 / rs;
+    for (int i = j + 1 + tid; i < n; i += kBlock) K[i * ld + j] *= inv;
+    if (tid == 0) s.diag[j] = rs;
+    __syncthreads();
+    const int m = n - j - 1;
+    for (int idx = tid; idx < m * m; idx += kBlock) {
+      const int r = idx / m, cc = idx - r * m;
+      if (cc <= r) {
+        const int i = j + 1 + r, k = j + 1 + cc;
+        K[i * ld + k] -= K[i * ld + j] * K[k * ld + j];
+      }
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
+// Solve L L' x = b for b in x[0..n) (LDS), by wave 0; rows lane and lane+64 live in registers.
+__device__ inline void chol_solve(const Lds& s, int n, int ld, double* x) {
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const int i0 = tid, i1 = tid + 64;
+    double b0 = i0 < n ? x[i0] : 0.0;
+    double b1 = i1 < n ? x[i1] : 0.0;
+    for (int j = 0; j < n; ++j) {
+      const double bj = j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64);
+      const double yj = bj / s.diag[j];
+      if (i0 == j) b0 = yj;
+      if (i1 == j) b1 = yj;
+      if (i0 > j && i0 < n) b0 -= s.K[i0 * ld + j] * yj;
+      if (i1 > j && i1 < n) b1 -= s.K[i1 * ld + j] * yj;
+    }
+    for (int j = n - 1; j >= 0; --j) {
+      const double yj = j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64);
+      const double xj = yj / s.diag[j];
+      if (i0 == j) b0 = xj;
+      if (i1 == j) b1 = xj;
+      if (i0 < j) b0 -= s.K[j * ld + i0] * xj;
+      if (i1 < j) b1 -= s.K[j * ld + i1] * xj;
+    }
+    if (i0 < n) x[i0] = b0;
+    if (i1 < n) x[i1] = b1;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row algebra.  An inequality row is G z + w = d with slack w >= 0 and dual lambda >= 0; for a
+// Newton step with complementarity target r_c the reduced quantities are
+//   D = lambda / w,  rho = D r_p + r_c / w,  dlambda = D (G dz) + rho,  dw = -r_p - G dz.
+// Affine step: r_c = -w lambda.  Corrector: r_c = -w lambda - dw_aff dlambda_aff + sigma mu.
+
+struct HsRow {
+  double h0, h1, g, sv, wA, lA, wB, lB;
+};
+struct HsLin {
+  double rpA, rpB, rds, DA, DB, sig;
+};
+struct RowDir {
+  double ds, dwA, dlA, dwB, dlB;
+};
+
+__device__ __forceinline__ HsLin hs_lin(const HsRow& q, double p0, double p1) {
+  HsLin l;
+  l.rpA = q.h0 * p0 + q.h1 * p1 + q.g - q.sv + q.wA;  // h.p + g - s + w_hs
+  l.rpB = q.wB - q.sv;                                // -s + w_s
+  l.rds = kSlackHess * q.sv + kSlackLin - q.lA - q.lB;
+  l.DA = q.lA / q.wA;
+  l.DB = q.lB / q.wB;
+  l.sig = kSlackHess + l.DA + l.DB;
+  return l;
+}
+
+// Slack eliminated per row: ds = (rhs_s + D_A h.dp) / sig with rhs_s = -r_ds + rho_A + rho_B.
+__device__ __forceinline__ RowDir hs_dir(const HsLin& l, double rhoA, double rhoB, double hdp) {
+  RowDir d;
+  d.ds = (-l.rds + rhoA + rhoB + l.DA * hdp) / l.sig;
+  // gA = h.dp - ds written without the cancellation of two ~D_A-sized terms
+  const double gA = (hdp * (kSlackHess + l.DB) + l.rds - rhoA - rhoB) / l.sig;
+  d.dwA = -l.rpA - gA;
+  d.dlA = l.DA * gA + rhoA;
+  d.dwB = -l.rpB + d.ds;
+  d.dlB = -l.DB * d.ds + rhoB;
+  return d;
+}
+
+__device__ __forceinline__ RowDir hs_affine(const HsRow& q, const HsLin& l, double hdpa) {
+  return hs_dir(l, l.DA * l.rpA - q.lA, l.DB * l.rpB - q.lB, hdpa);
+}
+
+__device__ __forceinline__ RowDir hs_corrector(const HsRow& q, const HsLin& l, double hdpa,
+                                               double hdp, double sigma_mu) {
+  const RowDir da = hs_affine(q, l, hdpa);
+  const double rhoA = l.DA * l.rpA - q.lA + (sigma_mu - da.dwA * da.dlA) / q.wA;
+  const double rhoB = l.DB * l.rpB - q.lB + (sigma_mu - da.dwB * da.dlB) / q.wB;
+  return hs_dir(l, rhoA, rhoB, hdp);
+}
+
+__device__ __forceinline__ double hs_ratio(const HsRow& q, const RowDir& d) {
+  return fmin(fmin(ratio(q.wA, d.dwA), ratio(q.lA, d.dlA)), fmin(ratio(q.wB, d.dwB), ratio(q.lB, d.dlB)));
+}
+
+// A two-sided bound lo <= y <= hi on a scalar y (an input or a position coordinate):
+//   upper row  y - hi + wu = 0 (G = +1),  lower row  lo - y + wl = 0 (G = -1).
+struct PairState {
+  double wu, lu, wl, ll;
+};
+struct PairDir {
+  double dwu, dlu, dwl, dll;
+};
+struct PairLin {
+  double rpu, rpl, Du, Dl;
+};
+__device__ __forceinline__ PairLin pair_lin(const PairState& q, double y, double lo, double hi) {
+  return {y - hi + q.wu, lo - y + q.wl, q.lu / q.wu, q.ll / q.wl};
+}
+__device__ __forceinline__ PairDir pair_dir(const PairState& q, const PairLin& l, double dya,
+                                            double dy, double sigma_mu, bool corrector) {
+  double rhou = l.Du * l.rpu - q.lu, rhol = l.Dl * l.rpl - q.ll;
+  if (corrector) {
+    const double dwu_a = -l.rpu - dya, dlu_a = l.Du * dya + rhou;
+    const double dwl_a = -l.rpl + dya, dll_a = -l.Dl * dya + rhol;
+    rhou += (sigma_mu - dwu_a * dlu_a) / q.wu;
+    rhol += (sigma_mu - dwl_a * dll_a) / q.wl;
+  }
+  return {-l.rpu - dy, l.Du * dy + rhou, -l.rpl + dy, -l.Dl * dy + rhol};
+}
+__device__ __forceinline__ double pair_ratio(const PairState& q, const PairDir& d) {
+  return fmin(fmin(ratio(q.wu, d.dwu), ratio(q.lu, d.dlu)), fmin(ratio(q.wl, d.dwl), ratio(q.ll, d.dll)));
+}
+// rho_u - rho_l of the affine step, and (base, unit) of the corrector split
+__device__ __forceinline__ double pair_rho_aff(const PairState& q, const PairLin& l) {
+  return (l.Du * l.rpu - q.lu) - (l.Dl * l.rpl - q.ll);
+}
+
+struct RowArrays {
+  double *h0, *h1, *g, *s, *wA, *lA, *wB, *lB;
+  __device__ __forceinline__ HsRow load(int64_t r) const {
+    return {h0[r], h1[r], g[r], s[r], wA[r], lA[r], wB[r], lB[r]};
+  }
+};
+
+__device__ __forceinline__ PairState box_state(const Lds& s, int n, int j) {
+  return {s.bx[j], s.bx[n + j], s.bx[2 * n + j], s.bx[3 * n + j]};
+}
+__device__ __forceinline__ PairState pos_state(const Lds& s, int H, int t) {
+  return {s.px[t], s.px[2 * H + t], s.px[4 * H + t], s.px[6 * H + t]};
+}
+
+// Sum kWaves per-step partials (wave 0, lane = step) in wave order.
+__device__ __forceinline__ double step_total(const double* red, int q, int lane) {
+  double t = red[q * 64 + lane];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) t += red[(w * kPerStepQ + q) * 64 + lane];
+  return t;
+}
+
+template <int NU>
+__global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
+  extern __shared__ double lds_raw[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  const int n = a.n, H = a.H, K = a.K, O = a.O, ld = a.ld, nx = a.nx;
+  const Lds s = carve(lds_raw, n, H, ld);
+  const double* H0 = a.blob + a.off.H0;
+  double* ws = a.ws + b * a.ws_pp;
+  const int64_t pitch = static_cast<int64_t>(O) * kStepPad;
+  const RowArrays rows{ws, ws + pitch, ws + 2 * pitch, ws + 3 * pitch,
+                       ws + 4 * pitch, ws + 5 * pitch, ws + 6 * pitch, ws + 7 * pitch};
+  const double* x0 = a.x0 + b * a.x0_sp;
+  const double* xr = a.xr + b * a.xr_sp;
+
+  // ------------------------------- setup -------------------------------
+  for (int t = tid; t < H * 2 * NU; t += kBlock) s.Mp[t] = a.blob[a.off.Mp + t];
+  for (int t = tid; t < 2 * H; t += kBlock) {
+    const double* ca = a.blob + a.off.CA + static_cast<int64_t>(t) * nx;
+    double acc = 0.0;
+    for (int q = 0; q < nx; ++q) acc += ca[q] * x0[q];
+    s.c[t] = acc;
+  }
+  for (int j = tid; j < n; j += kBlock) {
+    const double* f1 = a.blob + a.off.F1 + static_cast<int64_t>(j) * nx;
+    const double* f2 = a.blob + a.off.F2 + static_cast<int64_t>(j) * H * nx;
+    double acc = 0.0;
+    for (int q = 0; q < nx; ++q) acc += f1[q] * x0[q];
+    for (int t = 0; t < H; ++t)
+      for (int q = 0; q < nx; ++q) acc -= f2[t * nx + q] * xr[(t + 1) * a.xr_st + q];
+    s.f[j] = acc;
+    s.u[j] = 0.0;
+  }
+  __syncthreads();
+
+  // start: u = 0, s = 0, w = max(d - Gz, 1), lambda = 1 (same rule as the oracle)
+  double gmax = 0.0;
+  if (lane < K) {
+    const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
+    for (int o = wave; o < O; o += kWaves) {
+      const double* hp = a.hs_h + b * a.h_sp + o * a.h_so + lane * a.h_sk;
+      const double g = a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk];
+      const double h0 = hp[0], h1 = hp[1];
+      const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+      rows.h0[r] = h0;
+      rows.h1[r] = h1;
+      rows.g[r] = g;
+      rows.s[r] = 0.0;
+      rows.wA[r] = fmax(-(h0 * c0 + h1 * c1 + g), 1.0);
+      rows.lA[r] = 1.0;
+      rows.wB[r] = 1.0;
+      rows.lB[r] = 1.0;
+      gmax = fmax(gmax, fabs(g));
+    }
+  }
+  if (a.has_u) {
+    for (int j = tid; j < n; j += kBlock) {
+      const int ai = j % NU;
+      s.bx[j] = fmax(a.umax[ai], 1.0);
+      s.bx[n + j] = 1.0;
+      s.bx[2 * n + j] = fmax(-a.umin[ai], 1.0);
+      s.bx[3 * n + j] = 1.0;
+      gmax = fmax(gmax, fmax(fabs(a.umin[ai]), fabs(a.umax[ai])));
+    }
+  }
+  if (a.has_p) {
+    for (int t = tid; t < 2 * H; t += kBlock) {
+      const int i = t & 1;
+      s.px[t] = fmax(a.pmax[i] - s.c[t], 1.0);
+      s.px[2 * H + t] = 1.0;
+      s.px[4 * H + t] = fmax(s.c[t] - a.pmin[i], 1.0);
+      s.px[6 * H + t] = 1.0;
+      gmax = fmax(gmax, fmax(fabs(a.pmin[i]), fabs(a.pmax[i])));
+    }
+  }
+  double fmaxv = 0.0;
+  for (int j = tid; j < n; j += kBlock) fmaxv = fmax(fmaxv, fabs(s.f[j]));
+  {
+    double unused = 0.0;
+    block_sum_max_max(unused, gmax, fmaxv, s.sc);
+  }
+  const double scale_d = 1.0 + gmax;
+  const double scale_q = 1.0 + fmax(fmaxv, kSlackLin);
+  const double m_ineq = 2.0 * O * K + (a.has_u ? 2.0 * n : 0.0) + (a.has_p ? 4.0 * H : 0.0);
+
+  int status = DRCVAR_MPC_STATUS_MAX_ITER;
+  int it = 0, best_it = 0;
+  double mu = 0.0, rp = 0.0, rd = 0.0, best_merit = kHuge;
+  double* best_u = ws + kRowArrays * pitch;  // [n] best iterate
+  for (it = 1; it <= a.max_iter; ++it) {
+    // ---- positions of the iterate ----
+    positions<NU>(s, s.u, s.p, s.c, H);
+    __syncthreads();
+
+    // ---- P1: residuals, weights, per-step S / v / affine rhs ----
+    {
+      double acc[kPerStepQ] = {0, 0, 0, 0, 0, 0, 0};
+      double gap = 0.0, rpm = 0.0, rdm = 0.0;
+      if (lane < K) {
+        const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+        for (int o = wave; o < O; o += kWaves) {
+          const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+          const HsLin l = hs_lin(q, p0, p1);
+          const double om = l.DA * (kSlackHess + l.DB) / l.sig;
+          const double rhoA = l.DA * l.rpA - q.lA, rhoB = l.DB * l.rpB - q.lB;
+          const double coef = rhoA - l.DA * (-l.rds + rhoA + rhoB) / l.sig;
+          acc[0] += q.lA * q.h0;
+          acc[1] += q.lA * q.h1;
+          acc[2] += om * q.h0 * q.h0;
+          acc[3] += om * q.h0 * q.h1;
+          acc[4] += om * q.h1 * q.h1;
+          acc[5] += coef * q.h0;
+          acc[6] += coef * q.h1;
+          gap += q.wA * q.lA + q.wB * q.lB;
+          rpm = fmax(rpm, fmax(fabs(l.rpA), fabs(l.rpB)));
+          rdm = fmax(rdm, fabs(l.rds));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kPerStepQ; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+      __syncthreads();
+      if (wave == 0 && lane < H) {
+        double tot[kPerStepQ];
+#pragma unroll
+        for (int q = 0; q < kPerStepQ; ++q) tot[q] = lane < K ? step_total(s.red, q, lane) : 0.0;
+        if (a.has_p) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int t = 2 * lane + i;
+            const PairState q = pos_state(s, H, t);
+            const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
+            tot[i] += q.lu - q.ll;                    // v
+            tot[i == 0 ? 2 : 4] += l.Du + l.Dl;       // S diagonal
+            tot[5 + i] += pair_rho_aff(q, l);         // affine rhs
+            gap += q.wu * q.lu + q.wl * q.ll;
+            rpm = fmax(rpm, fmax(fabs(l.rpu), fabs(l.rpl)));
+          }
+        }
+        s.v[2 * lane] = tot[0];
+        s.v[2 * lane + 1] = tot[1];
+        s.S[lane] = tot[2];
+        s.S[H + lane] = tot[3];
+        s.S[2 * H + lane] = tot[4];
+        s.za[2 * lane] = tot[5];
+        s.za[2 * lane + 1] = tot[6];
+      }
+      for (int j = tid; j < n; j += kBlock) {
+        if (a.has_u) {
+          const int ai = j % NU;
+          const PairState q = box_state(s, n, j);
+          const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
+          s.DU[j] = l.Du + l.Dl;
+          s.rU[j] = pair_rho_aff(q, l);
+          gap += q.wu * q.lu + q.wl * q.ll;
+          rpm = fmax(rpm, fmax(fabs(l.rpu), fabs(l.rpl)));
+        } else {
+          s.DU[j] = 0.0;
+          s.rU[j] = 0.0;
+        }
+      }
+      __syncthreads();
+      // dual residual of the inputs: r_du = H0 u + f + Gp' v + (lUu - lUl)
+      for (int j = tid; j < n; j += kBlock) {
+        const double* h0r = H0 + static_cast<int64_t>(j) * n;
+        double r = s.f[j] + gp_transpose<NU>(s, s.v, j, H);
+        for (int l = 0; l < n; ++l) r += h0r[l] * s.u[l];
+        if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
+        s.rdu[j] = r;
+        rdm = fmax(rdm, fabs(r));
+      }
+      block_sum_max_max(gap, rpm, rdm, s.sc);
+      mu = m_ineq > 0.0 ? gap / m_ineq : 0.0;
+      rp = rpm;
+      rd = rdm;
+      if (!isfinite(gap) || !isfinite(rp) || !isfinite(rd)) {
+        status = DRCVAR_MPC_STATUS_NUMERICAL;
+        break;
+      }
+      const double merit = fmax(fmax(rp / scale_d, rd / scale_q), mu);
+      if (merit <= a.tol) {
+        status = DRCVAR_MPC_STATUS_OPTIMAL;
+        best_merit = merit;
+        break;
+      }
+      if (merit < best_merit) {  // uniform: every thread holds the same merit
+        best_merit = merit;
+        best_it = it;
+        for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];
+      }
+      if (best_merit < 1e-6 && it - best_it >= 8) break;  // stalled at the accuracy floor
+    }
+    const double gap = mu * m_ineq;
+
+    // ---- K = H0 + diag(DU) + sum_k Mp' S_k Mp, affine rhs ----
+    assemble_hessian<NU>(s, H0, n, ld, H);
+    for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - gp_transpose<NU>(s, s.za, j, H);
+    __syncthreads();
+    if (!cholesky(s, n, ld)) {
+      status = DRCVAR_MPC_STATUS_NUMERICAL;
+      break;
+    }
+    chol_solve(s, n, ld, s.dua);
+    positions<NU>(s, s.dua, s.dpa, nullptr, H);
+    __syncthreads();
+
+    // ---- P2: affine step length ----
+    double amax = kHuge;
+    if (lane < K) {
+      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+      const double d0 = s.dpa[2 * lane], d1 = s.dpa[2 * lane + 1];
+      for (int o = wave; o < O; o += kWaves) {
+        const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+        const HsLin l = hs_lin(q, p0, p1);
+        amax = fmin(amax, hs_ratio(q, hs_affine(q, l, q.h0 * d0 + q.h1 * d1)));
+      }
+    }
+    if (a.has_u) {
+      for (int j = tid; j < n; j += kBlock) {
+        const int ai = j % NU;
+        const PairState q = box_state(s, n, j);
+        const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
+        amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dua[j], 0.0, false)));
+      }
+    }
+    if (a.has_p) {
+      for (int t = tid; t < 2 * H; t += kBlock) {
+        const int i = t & 1;
+        const PairState q = pos_state(s, H, t);
+        const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
+        amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dpa[t], 0.0, false)));
+      }
+    }
+    const double a_aff = fmin(1.0, block_min(amax, s.sc));
+
+    // ---- P3: affine gap and the corrector rhs as base + sigma*mu * unit ----
+    {
+      double acc[4] = {0, 0, 0, 0};
+      double gap_aff = 0.0;
+      if (lane < K) {
+        const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+        const double d0 = s.dpa[2 * lane], d1 = s.dpa[2 * lane + 1];
+        for (int o = wave; o < O; o += kWaves) {
+          const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+          const HsLin l = hs_lin(q, p0, p1);
+          const RowDir d = hs_affine(q, l, q.h0 * d0 + q.h1 * d1);
+          gap_aff += (q.wA + a_aff * d.dwA) * (q.lA + a_aff * d.dlA) +
+                     (q.wB + a_aff * d.dwB) * (q.lB + a_aff * d.dlB);
+          const double rhoA_b = l.DA * l.rpA - q.lA - d.dwA * d.dlA / q.wA;
+          const double rhoB_b = l.DB * l.rpB - q.lB - d.dwB * d.dlB / q.wB;
+          const double cb = rhoA_b - l.DA * (-l.rds + rhoA_b + rhoB_b) / l.sig;
+          const double cu = 1.0 / q.wA - l.DA * (1.0 / q.wA + 1.0 / q.wB) / l.sig;
+          acc[0] += cb * q.h0;
+          acc[1] += cb * q.h1;
+          acc[2] += cu * q.h0;
+          acc[3] += cu * q.h1;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+      __syncthreads();
+      if (wave == 0 && lane < H) {
+        double tot[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tot[q] = lane < K ? step_total(s.red, q, lane) : 0.0;
+        if (a.has_p) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int t = 2 * lane + i;
+            const PairState q = pos_state(s, H, t);
+            const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
+            const PairDir d = pair_dir(q, l, 0.0, s.dpa[t], 0.0, false);
+            gap_aff += (q.wu + a_aff * d.dwu) * (q.lu + a_aff * d.dlu) +
+                       (q.wl + a_aff * d.dwl) * (q.ll + a_aff * d.dll);
+            tot[i] += (l.Du * l.rpu - q.lu - d.dwu * d.dlu / q.wu) -
+                      (l.Dl * l.rpl - q.ll - d.dwl * d.dll / q.wl);
+            tot[2 + i] += 1.0 / q.wu - 1.0 / q.wl;
+          }
+        }
+        s.za[2 * lane] = tot[0];
+        s.za[2 * lane + 1] = tot[1];
+        s.zu[2 * lane] = tot[2];
+        s.zu[2 * lane + 1] = tot[3];
+      }
+      for (int j = tid; j < n; j += kBlock) {
+        if (a.has_u) {
+          const int ai = j % NU;
+          const PairState q = box_state(s, n, j);
+          const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
+          const PairDir d = pair_dir(q, l, 0.0, s.dua[j], 0.0, false);
+          gap_aff += (q.wu + a_aff * d.dwu) * (q.lu + a_aff * d.dlu) +
+                     (q.wl + a_aff * d.dwl) * (q.ll + a_aff * d.dll);
+          s.rU[j] = (l.Du * l.rpu - q.lu - d.dwu * d.dlu / q.wu) -
+                    (l.Dl * l.rpl - q.ll - d.dwl * d.dll / q.wl);
+          s.rUu[j] = 1.0 / q.wu - 1.0 / q.wl;
+        } else {
+          s.rU[j] = 0.0;
+          s.rUu[j] = 0.0;
+        }
+      }
+      gap_aff = block_sum(gap_aff, s.sc);  // its barriers also publish za / zu / rU / rUu
+      const double ratio_g = gap > 0.0 ? gap_aff / gap : 0.0;
+      const double sigma_mu = ratio_g * ratio_g * ratio_g * mu;
+      s.sc[63] = sigma_mu;  // same value in every thread; kept for P4/P5
+      for (int j = tid; j < n; j += kBlock)
+        s.du[j] = -s.rdu[j] - (s.rU[j] + sigma_mu * s.rUu[j]) - gp_transpose<NU>(s, s.za, j, H) -
+                  sigma_mu * gp_transpose<NU>(s, s.zu, j, H);
+      __syncthreads();
+    }
+    const double sigma_mu = s.sc[63];
+    chol_solve(s, n, ld, s.du);
+    positions<NU>(s, s.du, s.dp, nullptr, H);
+    __syncthreads();
+
+    // ---- P4: corrector step length ----
+    amax = kHuge;
+    if (lane < K) {
+      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+      const double a0 = s.dpa[2 * lane], a1 = s.dpa[2 * lane + 1];
+      const double d0 = s.dp[2 * lane], d1 = s.dp[2 * lane + 1];
+      for (int o = wave; o < O; o += kWaves) {
+        const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+        const HsLin l = hs_lin(q, p0, p1);
+        amax = fmin(amax, hs_ratio(q, hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu)));
+      }
+    }
+    if (a.has_u) {
+      for (int j = tid; j < n; j += kBlock) {
+        const int ai = j % NU;
+        const PairState q = box_state(s, n, j);
+        const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
+        amax = fmin(amax, pair_ratio(q, pair_dir(q, l, s.dua[j], s.du[j], sigma_mu, true)));
+      }
+    }
+    if (a.has_p) {
+      for (int t = tid; t < 2 * H; t += kBlock) {
+        const int i = t & 1;
+        const PairState q = pos_state(s, H, t);
+        const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
+        amax = fmin(amax, pair_ratio(q, pair_dir(q, l, s.dpa[t], s.dp[t], sigma_mu, true)));
+      }
+    }
+    const double alpha = fmin(1.0, kStepFrac * block_min(amax, s.sc));
+
+    // ---- P5: update ----
+    if (lane < K) {
+      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+      const double a0 = s.dpa[2 * lane], a1 = s.dpa[2 * lane + 1];
+      const double d0 = s.dp[2 * lane], d1 = s.dp[2 * lane + 1];
+      for (int o = wave; o < O; o += kWaves) {
+        const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+        const HsRow q = rows.load(r);
+        const HsLin l = hs_lin(q, p0, p1);
+        const RowDir d = hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu);
+        rows.s[r] = q.sv + alpha * d.ds;
+        rows.wA[r] = q.wA + alpha * d.dwA;
+        rows.lA[r] = q.lA + alpha * d.dlA;
+        rows.wB[r] = q.wB + alpha * d.dwB;
+        rows.lB[r] = q.lB + alpha * d.dlB;
+      }
+    }
+    // box / position rows: every thread reads its own entries only, so no barrier is needed
+    // between computing the direction and writing the update
+    if (a.has_u) {
+      for (int j = tid; j < n; j += kBlock) {
+        const int ai = j % NU;
+        const PairState q = box_state(s, n, j);
+        const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
+        const PairDir d = pair_dir(q, l, s.dua[j], s.du[j], sigma_mu, true);
+        s.bx[j] = q.wu + alpha * d.dwu;
+        s.bx[n + j] = q.lu + alpha * d.dlu;
+        s.bx[2 * n + j] = q.wl + alpha * d.dwl;
+        s.bx[3 * n + j] = q.ll + alpha * d.dll;
+      }
+    }
+    if (a.has_p) {
+      for (int t = tid; t < 2 * H; t += kBlock) {
+        const int i = t & 1;
+        const PairState q = pos_state(s, H, t);
+        const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
+        const PairDir d = pair_dir(q, l, s.dpa[t], s.dp[t], sigma_mu, true);
+        s.px[t] = q.wu + alpha * d.dwu;
+        s.px[2 * H + t] = q.lu + alpha * d.dlu;
+        s.px[4 * H + t] = q.wl + alpha * d.dwl;
+        s.px[6 * H + t] = q.ll + alpha * d.dll;
+      }
+    }
+    __syncthreads();  // positions of the box loop read s.u; update it only after every reader
+    for (int j = tid; j < n; j += kBlock) s.u[j] += alpha * s.du[j];
+    __syncthreads();
+  }
+  if (it > a.max_iter) it = a.max_iter;
+  __syncthreads();
+  if (status != DRCVAR_MPC_STATUS_OPTIMAL && best_merit <= 1e3 * a.tol) {
+    // stalled close to the optimum: return the best iterate, its slacks re-optimised below
+    status = DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
+    for (int j = tid; j < n; j += kBlock) s.u[j] = best_u[j];
+  }
+
+  // ------------------------------- polish -------------------------------
+  // The interior-point iterate identifies the active set; the equality-constrained QP of that
+  // set is then solved by the method of multipliers (penalty kPolishRho, kPolishIters passes that
+  // reuse the Hessian assembly, the Cholesky and the triangular solves), and rows whose sign
+  // conditions fail are moved (primal-dual active-set step), up to kPolishAttempts times.  On
+  // success the answer is exact to roundoff; otherwise the interior-point answer stands.
+  int polish_attempts = 0;
+  bool polished = false;
+  if (a.polish && best_merit <= kPolishMerit && true) {
+    for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];  // the answer if polishing fails
+    // classify: flag 0 = halfspace not binding (s = 0), 1 = slack positive (s = h.p + g > 0),
+    // 2 = binding with s = 0 (equality, multiplier nu in [0, 50]); rows.s <- nu, rows.wA <- flag
+    if (lane < K) {
+      for (int o = wave; o < O; o += kWaves) {
+        const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+        const bool actA = rows.lA[r] > rows.wA[r], actB = rows.lB[r] > rows.wB[r];
+        const double flag = actA ? (actB ? 2.0 : 1.0) : 0.0;
+        rows.s[r] = flag == 2.0 ? rows.lA[r] : 0.0;
+        rows.wA[r] = flag;
+      }
+    }
+    // bounds: bx / px <- (flag_up, nu_up, flag_lo, nu_lo)
+    if (a.has_u) {
+      for (int j = tid; j < n; j += kBlock) {
+        const PairState q = box_state(s, n, j);
+        const bool up = q.lu > q.wu, lo = q.ll > q.wl;
+        s.bx[j] = up;
+        s.bx[n + j] = up ? q.lu : 0.0;
+        s.bx[2 * n + j] = lo;
+        s.bx[3 * n + j] = lo ? q.ll : 0.0;
+      }
+    }
+    if (a.has_p) {
+      for (int t = tid; t < 2 * H; t += kBlock) {
+        const PairState q = pos_state(s, H, t);
+        const bool up = q.lu > q.wu, lo = q.ll > q.wl;
+        s.px[t] = up;
+        s.px[2 * H + t] = up ? q.lu : 0.0;
+        s.px[4 * H + t] = lo;
+        s.px[6 * H + t] = lo ? q.ll : 0.0;
+      }
+    }
+    __syncthreads();
+    const double tolf = 1e-9 * scale_d;
+    for (int attempt = 0; attempt < kPolishAttempts && !polished; ++attempt) {
+      ++polish_attempts;
+      // Hessian of the active-set problem: 100 h h' for positive slacks, rho h h' for equalities
+      {
+        double acc[3] = {0, 0, 0};
+        if (lane < K) {
+          for (int o = wave; o < O; o += kWaves) {
+            const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+            const double flag = rows.wA[r];
+            const double wgt = flag == 1.0 ? kSlackHess : (flag == 2.0 ? kPolishRho : 0.0);
+            const double h0 = rows.h0[r], h1 = rows.h1[r];
+            acc[0] += wgt * h0 * h0;
+            acc[1] += wgt * h0 * h1;
+            acc[2] += wgt * h1 * h1;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+        __syncthreads();
+        if (wave == 0 && lane < H) {
+          double t0 = lane < K ? step_total(s.red, 0, lane) : 0.0;
+          const double t1 = lane < K ? step_total(s.red, 1, lane) : 0.0;
+          double t2 = lane < K ? step_total(s.red, 2, lane) : 0.0;
+          if (a.has_p) {
+            t0 += kPolishRho * (s.px[2 * lane] + s.px[4 * H + 2 * lane]);
+            t2 += kPolishRho * (s.px[2 * lane + 1] + s.px[4 * H + 2 * lane + 1]);
+          }
+          s.S[lane] = t0;
+          s.S[H + lane] = t1;
+          s.S[2 * H + lane] = t2;
+        }
+        for (int j = tid; j < n; j += kBlock)
+          s.DU[j] = a.has_u ? kPolishRho * (s.bx[j] + s.bx[2 * n + j]) : 0.0;
+        __syncthreads();
+      }
+      assemble_hessian<NU>(s, H0, n, ld, H);
+      __syncthreads();
+      if (!cholesky(s, n, ld)) break;
+      for (int pass = 0; pass < kPolishIters; ++pass) {
+        // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
+        double acc[2] = {0, 0};
+        if (lane < K) {
+          const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
+          for (int o = wave; o < O; o += kWaves) {
+            const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+            const double flag = rows.wA[r];
+            const double h0 = rows.h0[r], h1 = rows.h1[r];
+            const double bb = h0 * c0 + h1 * c1 + rows.g[r];
+            const double coef = flag == 1.0 ? kSlackLin + kSlackHess * bb
+                                            : (flag == 2.0 ? rows.s[r] + kPolishRho * bb : 0.0);
+            acc[0] += coef * h0;
+            acc[1] += coef * h1;
+          }
+        }
+        s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];
+        s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
+        __syncthreads();
+        if (wave == 0 && lane < H) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int t = 2 * lane + i;
+            double z = lane < K ? step_total(s.red, i, lane) : 0.0;
+            if (a.has_p) {
+              if (s.px[t] != 0.0) z += s.px[2 * H + t] - kPolishRho * (a.pmax[i] - s.c[t]);
+              if (s.px[4 * H + t] != 0.0) z -= s.px[6 * H + t] - kPolishRho * (s.c[t] - a.pmin[i]);
+            }
+            s.za[t] = z;
+          }
+        }
+        __syncthreads();
+        for (int j = tid; j < n; j += kBlock) {
+          double r = -s.f[j] - gp_transpose<NU>(s, s.za, j, H);
+          if (a.has_u) {
+            const int ai = j % NU;
+            if (s.bx[j] != 0.0) r -= s.bx[n + j] - kPolishRho * a.umax[ai];
+            if (s.bx[2 * n + j] != 0.0) r += s.bx[3 * n + j] + kPolishRho * a.umin[ai];
+          }
+          s.du[j] = r;
+        }
+        __syncthreads();
+        chol_solve(s, n, ld, s.du);
+        for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
+        __syncthreads();
+        positions<NU>(s, s.u, s.p, s.c, H);
+        __syncthreads();
+        // multiplier updates nu += rho * (E u - e)
+        if (lane < K) {
+          const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+          for (int o = wave; o < O; o += kWaves) {
+            const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+            if (rows.wA[r] == 2.0) rows.s[r] += kPolishRho * (rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r]);
+          }
+        }
+        if (a.has_u) {
+          for (int j = tid; j < n; j += kBlock) {
+            const int ai = j % NU;
+            if (s.bx[j] != 0.0) s.bx[n + j] += kPolishRho * (s.u[j] - a.umax[ai]);
+            if (s.bx[2 * n + j] != 0.0) s.bx[3 * n + j] += kPolishRho * (a.umin[ai] - s.u[j]);
+          }
+        }
+        if (a.has_p) {
+          for (int t = tid; t < 2 * H; t += kBlock) {
+            const int i = t & 1;
+            if (s.px[t] != 0.0) s.px[2 * H + t] += kPolishRho * (s.p[t] - a.pmax[i]);
+            if (s.px[4 * H + t] != 0.0) s.px[6 * H + t] += kPolishRho * (a.pmin[i] - s.p[t]);
+          }
+        }
+        __syncthreads();
+      }
+      // sign conditions; violators move (primal-dual active-set step)
+      double bad = 0.0;
+      if (lane < K) {
+        const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+        for (int o = wave; o < O; o += kWaves) {
+          const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+          const double flag = rows.wA[r];
+          const double hp = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
+          double nf = flag, nv = rows.s[r];
+          if (flag == 2.0) {
+            if (nv > kSlackLin + kPolishDualTol) nf = 1.0;        // the slack is positive after all
+            else if (nv < -kPolishDualTol) nf = 0.0;              // not binding
+            nv = nf == 2.0 ? fmin(fmax(nv, 0.0), kSlackLin) : 0.0;
+          } else if (flag == 1.0) {
+            if (hp < -tolf) { nf = 2.0; nv = 0.0; }               // penalised row with s < 0
+          } else if (hp > tolf) {
+            nf = 2.0;                                             // dropped row violated
+            nv = 0.0;
+          }
+          bad += nf != flag;
+          rows.wA[r] = nf;
+          rows.s[r] = nv;
+        }
+      }
+      if (a.has_u) {
+        for (int j = tid; j < n; j += kBlock) {
+          const int ai = j % NU;
+          const double uj = s.u[j];
+          for (int side = 0; side < 2; ++side) {
+            double* fl = s.bx + 2 * side * n + j;
+            double* nv = fl + n;
+            const double viol = side == 0 ? uj - a.umax[ai] : a.umin[ai] - uj;
+            if (*fl != 0.0 && *nv < -kPolishDualTol) { *fl = 0.0; *nv = 0.0; bad += 1.0; }
+            else if (*fl == 0.0 && viol > tolf) { *fl = 1.0; *nv = 0.0; bad += 1.0; }
+            else if (*fl != 0.0) *nv = fmax(*nv, 0.0);
+          }
+        }
+      }
+      if (a.has_p) {
+        for (int t = tid; t < 2 * H; t += kBlock) {
+          const int i = t & 1;
+          const double pv = s.p[t];
+          for (int side = 0; side < 2; ++side) {
+            double* fl = s.px + 4 * side * H + t;
+            double* nv = fl + 2 * H;
+            const double viol = side == 0 ? pv - a.pmax[i] : a.pmin[i] - pv;
+            if (*fl != 0.0 && *nv < -kPolishDualTol) { *fl = 0.0; *nv = 0.0; bad += 1.0; }
+            else if (*fl == 0.0 && viol > tolf) { *fl = 1.0; *nv = 0.0; bad += 1.0; }
+            else if (*fl != 0.0) *nv = fmax(*nv, 0.0);
+          }
+        }
+      }
+      bad = block_sum(bad, s.sc);
+      if (bad == 0.0) polished = true;
+    }
+    if (polished) {
+      status = DRCVAR_MPC_STATUS_OPTIMAL;
+    } else {
+      for (int j = tid; j < n; j += kBlock) s.u[j] = best_u[j];
+    }
+    __syncthreads();
+  }
+
+  // ------------------------------- output -------------------------------
+  const bool optimal = status == DRCVAR_MPC_STATUS_OPTIMAL || status == DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
+  if (!optimal) {
+    const double* uf = a.uf + b * a.uf_sp;
+    for (int j = tid; j < n; j += kBlock) s.u[j] = uf[(j / NU) * a.uf_st + j % NU];
+  }
+  for (int q = tid; q < nx; q += kBlock) s.xs[q] = x0[q];
+  __syncthreads();
+  positions<NU>(s, s.u, s.p, s.c, H);  // positions of the returned inputs (slacks below)
+  const double* A = a.blob + a.off.A;
+  const double* B = a.blob + a.off.B;
+  for (int t = 0; t < H; ++t) {  // x_{t+1} = A x_t + B u_t (core/mpc_filter.py:85-86, :216-217)
+    if (tid < nx) {
+      double acc = 0.0;
+      for (int q = 0; q < nx; ++q) acc += A[tid * nx + q] * s.xs[t * nx + q];
+      for (int q = 0; q < NU; ++q) acc += B[tid * NU + q] * s.u[t * NU + q];
+      s.xs[(t + 1) * nx + tid] = acc;
+    }
+    __syncthreads();
+  }
+  // objective (core/mpc_filter.py:64-76,142-144) and the largest slack
+  double obj = 0.0, smax = 0.0;
+  if (optimal) {
+    const double* Q = a.blob + a.off.Q;
+    const double* R = a.blob + a.off.R;
+    for (int t = tid; t < H; t += kBlock) {
+      double e[DRCVAR_MPC_MAX_STATES];
+      for (int q = 0; q < nx; ++q) e[q] = s.xs[(t + 1) * nx + q] - xr[(t + 1) * a.xr_st + q];
+      for (int q = 0; q < nx; ++q) {
+        double row = 0.0;
+        for (int r = 0; r < nx; ++r) row += Q[q * nx + r] * e[r];
+        obj += e[q] * row;
+      }
+      for (int q = 0; q < NU; ++q) {
+        double row = 0.0;
+        for (int r = 0; r < NU; ++r) row += R[q * NU + r] * s.u[t * NU + r];
+        obj += s.u[t * NU + q] * row;
+      }
+    }
+    if (lane < K) {
+      // the optimal slack of a halfspace for the returned inputs is max(0, h.p + g)
+      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+      for (int o = wave; o < O; o += kWaves) {
+        const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+        const double sv = fmax(0.0, rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r]);
+        rows.s[r] = sv;
+        obj += kSlackLin * sv + 0.5 * kSlackHess * sv * sv;
+        smax = fmax(smax, sv);
+      }
+    }
+  }
+  double unused = 0.0;
+  block_sum_max_max(obj, smax, unused, s.sc);
+  double* xo = a.x_out + b * (H + 1) * nx;
+  for (int q = tid; q < (H + 1) * nx; q += kBlock) xo[q] = s.xs[q];
+  double* uo = a.u_out + b * n;
+  for (int j = tid; j < n; j += kBlock) uo[j] = s.u[j];
+  if (tid == 0) {
+    double* info = a.info + b * DRCVAR_MPC_INFO_WIDTH;
+    info[DRCVAR_MPC_INFO_STATUS] = status;
+    info[DRCVAR_MPC_INFO_ITERATIONS] = it;
+    info[DRCVAR_MPC_INFO_OBJECTIVE] = optimal ? obj : NAN;
+    info[DRCVAR_MPC_INFO_MU] = best_merit;
+    info[DRCVAR_MPC_INFO_PRIMAL_RES] = rp;
+    info[DRCVAR_MPC_INFO_DUAL_RES] = rd;
+    info[DRCVAR_MPC_INFO_MAX_SLACK] = optimal ? smax : NAN;
+    info[DRCVAR_MPC_INFO_USED_FALLBACK] = optimal ? 0.0 : 1.0;
+    info[DRCVAR_MPC_INFO_POLISHED] = polished ? 1.0 : 0.0;
+    info[DRCVAR_MPC_INFO_POLISH_ATTEMPTS] = polish_attempts;
+  }
+}
+
+// ------------------------------- host side -------------------------------
+
+bool all_finite(const double* p, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (!std::isfinite(p[i])) return false;
+  return true;
+}
+
+template <int NU>
+int launch(const MpcArgs& args, int64_t n_problems, size_t lds_bytes, hipStream_t stream) {
+  static bool attr_set = false;  // idempotent; a racing second call sets the same value
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return DRCVAR_ERR_LAUNCH;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(mpc_ipm_kernel<NU>, dim3(static_cast<unsigned>(n_problems)), dim3(kBlock),
+                     lds_bytes, stream, args);
+  return DRCVAR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int drcvar_mpc_model_init(const double* A, const double* B, const double* C, const double* Q,
+                          const double* R, int32_t nx, int32_t nu, int32_t ny, int32_t H,
+                          const double* u_min, const double* u_max, const double* p_min,
+                          const double* p_max, drcvar_mpc_model* model, double* blob) {
+  if (!A || !B || !C || !Q || !R || !model) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (nx < 1 || nu < 1 || H < 1 || ny != 2) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (nx > DRCVAR_MPC_MAX_STATES || nu > DRCVAR_MPC_MAX_INPUTS || H > DRCVAR_MPC_MAX_HORIZON ||
+      nu * H > DRCVAR_MPC_MAX_DECISION)
+    return DRCVAR_ERR_UNSUPPORTED;
+  if ((u_min == nullptr) != (u_max == nullptr) || (p_min == nullptr) != (p_max == nullptr))
+    return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (!all_finite(A, nx * nx) || !all_finite(B, nx * nu) || !all_finite(C, ny * nx) ||
+      !all_finite(Q, nx * nx) || !all_finite(R, nu * nu))
+    return DRCVAR_ERR_INVALID_ARGUMENT;
+  drcvar_mpc_model m{};
+  m.n_states = nx;
+  m.n_inputs = nu;
+  m.n_outputs = ny;
+  m.horizon = H;
+  m.has_input_bounds = u_min != nullptr;
+  m.has_position_bounds = p_min != nullptr;
+  for (int i = 0; i < nu && u_min; ++i) {
+    m.u_min[i] = u_min[i];
+    m.u_max[i] = u_max[i];
+    if (!std::isfinite(u_min[i]) || !std::isfinite(u_max[i])) return DRCVAR_ERR_INVALID_ARGUMENT;
+  }
+  for (int i = 0; i < 2 && p_min; ++i) {
+    m.p_min[i] = p_min[i];
+    m.p_max[i] = p_max[i];
+    if (!std::isfinite(p_min[i]) || !std::isfinite(p_max[i])) return DRCVAR_ERR_INVALID_ARGUMENT;
+  }
+  const BlobLayout L = blob_layout(nx, nu, H);
+  m.blob_doubles = L.total;
+  *model = m;
+  if (!blob) return DRCVAR_OK;
+
+  const int n = nu * H;
+  // A^i for i = 0..H, row-major nx x nx
+  std::vector<double> Apow(static_cast<size_t>(H + 1) * nx * nx, 0.0);
+  for (int i = 0; i < nx; ++i) Apow[i * nx + i] = 1.0;
+  for (int p = 1; p <= H; ++p) {
+    const double* prev = &Apow[static_cast<size_t>(p - 1) * nx * nx];
+    double* cur = &Apow[static_cast<size_t>(p) * nx * nx];
+    for (int i = 0; i < nx; ++i)
+      for (int j = 0; j < nx; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < nx; ++k) acc += A[i * nx + k] * prev[k * nx + j];
+        cur[i * nx + j] = acc;
+      }
+  }
+  // AB[i] = A^i B  (nx x nu)
+  std::vector<double> AB(static_cast<size_t>(H) * nx * nu, 0.0);
+  for (int p = 0; p < H; ++p)
+    for (int i = 0; i < nx; ++i)
+      for (int j = 0; j < nu; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < nx; ++k) acc += Apow[(static_cast<size_t>(p) * nx + i) * nx + k] * B[k * nu + j];
+        AB[(static_cast<size_t>(p) * nx + i) * nu + j] = acc;
+      }
+  // Gx: x_{k+1} = A^{k+1} x0 + sum_{j<=k} A^{k-j} B u_j  -> Gx [(H*nx) x n], Phi [(H*nx) x nx]
+  std::vector<double> Gx(static_cast<size_t>(H) * nx * n, 0.0);
+  for (int k = 0; k < H; ++k)
+    for (int j = 0; j <= k; ++j)
+      for (int i = 0; i < nx; ++i)
+        for (int c = 0; c < nu; ++c)
+          Gx[(static_cast<size_t>(k) * nx + i) * n + j * nu + c] = AB[(static_cast<size_t>(k - j) * nx + i) * nu + c];
+  // QG = blockdiag(Q) Gx
+  std::vector<double> QG(Gx.size(), 0.0);
+  for (int k = 0; k < H; ++k)
+    for (int i = 0; i < nx; ++i)
+      for (int c = 0; c < n; ++c) {
+        double acc = 0.0;
+        for (int q = 0; q < nx; ++q) acc += Q[i * nx + q] * Gx[(static_cast<size_t>(k) * nx + q) * n + c];
+        QG[(static_cast<size_t>(k) * nx + i) * n + c] = acc;
+      }
+  double* H0 = blob + L.H0;
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) {
+      double acc = 0.0;
+      for (int t = 0; t < H * nx; ++t) acc += Gx[static_cast<size_t>(t) * n + r] * QG[static_cast<size_t>(t) * n + c];
+      H0[r * n + c] = 2.0 * acc;
+    }
+  for (int t = 0; t < H; ++t)
+    for (int i = 0; i < nu; ++i)
+      for (int j = 0; j < nu; ++j) H0[(t * nu + i) * n + t * nu + j] += 2.0 * R[i * nu + j];
+  // F1 = 2 Gx' Qbar Phi  (n x nx),  F2 = 2 Gx' Qbar (n x H*nx)
+  double* F1 = blob + L.F1;
+  double* F2 = blob + L.F2;
+  for (int r = 0; r < n; ++r) {
+    for (int c = 0; c < nx; ++c) {
+      double acc = 0.0;
+      for (int k = 0; k < H; ++k)
+        for (int i = 0; i < nx; ++i)
+          acc += QG[(static_cast<size_t>(k) * nx + i) * n + r] * Apow[(static_cast<size_t>(k + 1) * nx + i) * nx + c];
+      F1[r * nx + c] = 2.0 * acc;
+    }
+    for (int t = 0; t < H * nx; ++t) F2[static_cast<size_t>(r) * H * nx + t] = 2.0 * QG[static_cast<size_t>(t) * n + r];
+  }
+  // Mp[i] = C A^i B (2 x nu),  CA[k] = C A^{k+1} (2 x nx)
+  for (int p = 0; p < H; ++p)
+    for (int i = 0; i < 2; ++i) {
+      for (int j = 0; j < nu; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < nx; ++k) acc += C[i * nx + k] * AB[(static_cast<size_t>(p) * nx + k) * nu + j];
+        blob[L.Mp + (p * 2 + i) * nu + j] = acc;
+      }
+      for (int j = 0; j < nx; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < nx; ++k) acc += C[i * nx + k] * Apow[(static_cast<size_t>(p + 1) * nx + k) * nx + j];
+        blob[L.CA + (p * 2 + i) * nx + j] = acc;
+      }
+    }
+  std::memcpy(blob + L.A, A, sizeof(double) * nx * nx);
+  std::memcpy(blob + L.B, B, sizeof(double) * nx * nu);
+  std::memcpy(blob + L.Q, Q, sizeof(double) * nx * nx);
+  std::memcpy(blob + L.R, R, sizeof(double) * nu * nu);
+  return DRCVAR_OK;
+}
+
+int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_problems,
+                                     int64_t n_obstacles) {
+  if (!model || n_problems < 0 || n_obstacles < 0) return -1;
+  return n_problems * (kRowArrays * n_obstacles * kStepPad + kBestPad);
+}
+
+int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
+                          const double* hs_h, const double* hs_g, int64_t n_obstacles,
+                          int64_t n_hs_steps, int64_t h_sp, int64_t h_so, int64_t h_sk,
+                          int64_t g_sp, int64_t g_so, int64_t g_sk, const double* x0,
+                          int64_t x0_sp, const double* x_ref, int64_t xr_sp, int64_t xr_st,
+                          const double* u_fallback, int64_t uf_sp, int64_t uf_st, int32_t max_iter,
+                          double tol, int32_t polish, double* x_out, double* u_out, double* info_out,
+                          double* workspace, int64_t workspace_doubles, void* stream) {
+  if (!model || !blob || n_problems < 0 || n_obstacles < 0 || n_hs_steps < 0)
+    return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (n_problems == 0) return DRCVAR_OK;
+  if (!x0 || !x_ref || !u_fallback || !x_out || !u_out || !info_out) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (max_iter < 1 || !(tol > 0.0) || n_problems > 0x7fffffffLL) return DRCVAR_ERR_INVALID_ARGUMENT;
+  const int nx = model->n_states, nu = model->n_inputs, H = model->horizon;
+  if (nx < 1 || nx > DRCVAR_MPC_MAX_STATES || nu < 1 || nu > DRCVAR_MPC_MAX_INPUTS || H < 1 ||
+      H > DRCVAR_MPC_MAX_HORIZON || nu * H > DRCVAR_MPC_MAX_DECISION || model->n_outputs != 2)
+    return DRCVAR_ERR_INVALID_ARGUMENT;
+  const int64_t K = n_hs_steps < H ? n_hs_steps : H;
+  if (K > 0 && n_obstacles > 0 && (!hs_h || !hs_g)) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (n_obstacles > (int64_t{1} << 24)) return DRCVAR_ERR_UNSUPPORTED;
+  const int64_t need = drcvar_mpc_workspace_doubles(model, n_problems, n_obstacles);
+  if (!workspace || workspace_doubles < need) return DRCVAR_ERR_INVALID_ARGUMENT;
+
+  MpcArgs args{};
+  args.blob = blob;
+  args.off = blob_layout(nx, nu, H);
+  args.nx = nx;
+  args.nu = nu;
+  args.H = H;
+  args.n = nu * H;
+  args.K = static_cast<int>(K);
+  args.O = static_cast<int>(n_obstacles);
+  args.ld = args.n | 1;  // odd leading dimension: column walks hit distinct LDS banks
+  args.has_u = model->has_input_bounds;
+  args.has_p = model->has_position_bounds;
+  for (int i = 0; i < DRCVAR_MPC_MAX_INPUTS; ++i) {
+    args.umin[i] = model->u_min[i];
+    args.umax[i] = model->u_max[i];
+  }
+  for (int i = 0; i < 2; ++i) {
+    args.pmin[i] = model->p_min[i];
+    args.pmax[i] = model->p_max[i];
+  }
+  args.hs_h = hs_h;
+  args.hs_g = hs_g;
+  args.h_sp = h_sp;
+  args.h_so = h_so;
+  args.h_sk = h_sk;
+  args.g_sp = g_sp;
+  args.g_so = g_so;
+  args.g_sk = g_sk;
+  args.x0 = x0;
+  args.x0_sp = x0_sp;
+  args.xr = x_ref;
+  args.xr_sp = xr_sp;
+  args.xr_st = xr_st;
+  args.uf = u_fallback;
+  args.uf_sp = uf_sp;
+  args.uf_st = uf_st;
+  args.x_out = x_out;
+  args.u_out = u_out;
+  args.info = info_out;
+  args.ws = workspace;
+  args.ws_pp = kRowArrays * n_obstacles * kStepPad + kBestPad;
+  args.max_iter = max_iter;
+  args.tol = tol;
+  args.polish = polish;
+  const size_t lds_bytes = sizeof(double) * static_cast<size_t>(lds_doubles(args.n, H, args.ld));
+  if (lds_bytes > 160 * 1024) return DRCVAR_ERR_UNSUPPORTED;
+
+  (void)hipGetLastError();
+  auto st = static_cast<hipStream_t>(stream);
+  int rc;
+  switch (nu) {
+    case 1: rc = launch<1>(args, n_problems, lds_bytes, st); break;
+    case 2: rc = launch<2>(args, n_problems, lds_bytes, st); break;
+    case 3: rc = launch<3>(args, n_problems, lds_bytes, st); break;
+    default: rc = launch<4>(args, n_problems, lds_bytes, st); break;
+  }
+  if (rc != DRCVAR_OK) return rc;
+  return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
+}
+
+}  // extern "C"

@@ -19,7 +19,9 @@ def pytest_configure(config):
 
 
 def golden_files():
-    return sorted(glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    """Halfspace fixtures (the mpc_*.npz hand-off fixtures are loaded by tests/test_mpc.py)."""
+    return sorted(p for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                  if not os.path.basename(p).startswith("mpc_"))
 
 
 def load_golden(path):

@@ -10,13 +10,15 @@ import pytest
 from conftest import REPO
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
 
-HEADER = os.path.join(REPO, "include", "drcvar_halfspace.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("drcvar_halfspace.h", "drcvar_mpc.h")]
 
 
 def _declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(drcvar_\w+)\s*\(", text, flags=re.M)))
+    names = set()
+    for header in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(header).read(), flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(drcvar_\w+)\s*\(", text, flags=re.M))
+    return sorted(names)
 
 
 def test_header_declares_the_bound_symbols():
