@@ -57,6 +57,24 @@ constexpr int kPolishAttempts = 4;    // active-set corrections
 constexpr double kPolishMerit = 1e-6; // polish only from an iterate this close to the optimum
 constexpr double kPolishDualTol = 1e-7;
 
+#ifdef DRCVAR_MPC_STAMPS
+// diagnostic build only: per-category shader-clock totals of problem 0..kStampProblems-1
+constexpr int kStampProblems = 64, kStampSlots = 16;
+__device__ unsigned long long g_mpc_stamps[kStampProblems * kStampSlots];
+#define MPC_PHASE(k)                                                    \
+  do {                                                                  \
+    if (threadIdx.x == 0) {                                             \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+      stamp_acc[(k)] += now_ - stamp_last;                              \
+      stamp_last = now_;                                                \
+    }                                                                   \
+  } while (0)
+#else
+#define MPC_PHASE(k) \
+  do {               \
+  } while (0)
+#endif
+
 struct BlobLayout {
   int64_t H0, F1, F2, Mp, CA, A, B, Q, R, total;
 };
@@ -304,57 +322,106 @@ __device__ inline void assemble_hessian(const Lds& s, const double* H0, int n, i
   }
 }
 
-// Right-looking Cholesky of the lower triangle of K (n x n, leading dimension ld), in place;
-// s.diag[j] = L_jj.  Two barriers per column.  Returns false on a non-positive/non-finite pivot.
+// Right-looking LDL' factorisation of the lower triangle of K (n x n, leading dimension ld), in
+// place, with UNSCALED columns: afterwards K[i][j] (i > j) = L_ij d_j and s.diag[j] = 1 / d_j.
+// Keeping the columns unscaled lets step j read column j while the trailing update writes only
+// columns > j, so each column costs ONE barrier.  Two threads per trailing column (even / odd
+// rows); each thread issues its loads in groups of four before the dependent stores, so the LDS
+// latency is paid once per group.  Returns false on a non-positive or non-finite pivot (uniform).
 __device__ inline bool cholesky(const Lds& s, int n, int ld) {
   const int tid = threadIdx.x;
   double* K = s.K;
+  const int col_off = tid & 127, half = tid >> 7;
+  static_assert(kBlock == 256 && DRCVAR_MPC_MAX_DECISION <= 128, "two threads per column");
   for (int j = 0; j < n; ++j) {
     const double d = K[j * ld + j];
-    if (!(d > 0.0) || !isfinite(d)) return false;  // uniform: every thread read the same value
-    const double rs = sqrt(d);
-    const double inv = 1.0 / rs;
-    for (int i = j + 1 + tid; i < n; i += kBlock) K[i * ld + j] *= inv;
-    if (tid == 0) s.diag[j] = rs;
-    __syncthreads();
-    const int m = n - j - 1;
-    for (int idx = tid; idx < m * m; idx += kBlock) {
-      const int r = idx / m, cc = idx - r * m;
-      if (cc <= r) {
-        const int i = j + 1 + r, k = j + 1 + cc;
-        K[i * ld + k] -= K[i * ld + j] * K[k * ld + j];
+    if (!(d > 0.0) || !isfinite(d)) return false;
+    const double invd = 1.0 / d;
+    if (tid == 0) s.diag[j] = invd;
+    const int k = j + 1 + col_off;
+    if (k < n) {
+      const double lkj = K[k * ld + j] * invd;
+      int i = k + half;
+      for (; i + 6 < n; i += 8) {
+        double a[4], c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[q] = K[(i + 2 * q) * ld + j];
+          c[q] = K[(i + 2 * q) * ld + k];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) K[(i + 2 * q) * ld + k] = c[q] - a[q] * lkj;
       }
+      for (; i < n; i += 2) K[i * ld + k] -= K[i * ld + j] * lkj;
     }
     __syncthreads();
   }
   return true;
 }
 
-// Solve L L' x = b for b in x[0..n) (LDS), by wave 0; rows lane and lane+64 live in registers.
+// Solve K x = b with the factor above, b in x[0..n) (LDS), by wave 0; rows lane and lane + 64
+// live in registers and the pivot value travels by readlane.  The LDS operands are loaded eight
+// steps at a time, so the LDS latency is paid once per eight steps and the dependent chain per
+// step is readlane -> mul -> fma.
+constexpr int kSolveBlock = 8;
+
 __device__ inline void chol_solve(const Lds& s, int n, int ld, double* x) {
   const int tid = threadIdx.x;
   if (tid < 64) {
+    const double* K = s.K;
     const int i0 = tid, i1 = tid + 64;
-    double b0 = i0 < n ? x[i0] : 0.0;
-    double b1 = i1 < n ? x[i1] : 0.0;
-    for (int j = 0; j < n; ++j) {
-      const double bj = j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64);
-      const double yj = bj / s.diag[j];
-      if (i0 == j) b0 = yj;
-      if (i1 == j) b1 = yj;
-      if (i0 > j && i0 < n) b0 -= s.K[i0 * ld + j] * yj;
-      if (i1 > j && i1 < n) b1 -= s.K[i1 * ld + j] * yj;
+    const bool v0 = i0 < n, v1 = i1 < n;
+    double b0 = v0 ? x[i0] : 0.0;
+    double b1 = v1 ? x[i1] : 0.0;
+    // forward: z_j = b_j / d_j, b_i -= C_ij z_j  (C = L D, unit-lower L)
+    for (int jb = 0; jb < n; jb += kSolveBlock) {
+      double c0[kSolveBlock], c1[kSolveBlock], dv[kSolveBlock];
+#pragma unroll
+      for (int q = 0; q < kSolveBlock; ++q) {
+        const int j = jb + q < n ? jb + q : n - 1;
+        c0[q] = v0 ? K[i0 * ld + j] : 0.0;
+        c1[q] = v1 ? K[i1 * ld + j] : 0.0;
+        dv[q] = s.diag[j];
+      }
+#pragma unroll
+      for (int q = 0; q < kSolveBlock; ++q) {
+        const int j = jb + q;
+        if (j < n) {
+          const double zj = (j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64)) * dv[q];
+          if (i0 == j) b0 = zj;
+          if (i1 == j) b1 = zj;
+          if (i0 > j) b0 -= c0[q] * zj;
+          if (i1 > j) b1 -= c1[q] * zj;
+        }
+      }
     }
-    for (int j = n - 1; j >= 0; --j) {
-      const double yj = j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64);
-      const double xj = yj / s.diag[j];
-      if (i0 == j) b0 = xj;
-      if (i1 == j) b1 = xj;
-      if (i0 < j) b0 -= s.K[j * ld + i0] * xj;
-      if (i1 < j) b1 -= s.K[j * ld + i1] * xj;
+    // backward: x_j = z_j - (sum_{i>j} C_ij x_i) / d_j, accumulated row by row
+    double a0 = 0.0, a1 = 0.0;
+    for (int jt = n - 1; jt >= 0; jt -= kSolveBlock) {
+      double r0[kSolveBlock], r1[kSolveBlock], dv[kSolveBlock];
+#pragma unroll
+      for (int q = 0; q < kSolveBlock; ++q) {
+        const int j = jt - q >= 0 ? jt - q : 0;
+        r0[q] = i0 < j ? K[j * ld + i0] : 0.0;
+        r1[q] = i1 < j ? K[j * ld + i1] : 0.0;
+        dv[q] = s.diag[j];
+      }
+#pragma unroll
+      for (int q = 0; q < kSolveBlock; ++q) {
+        const int j = jt - q;
+        if (j >= 0) {
+          const double zj = j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64);
+          const double aj = j < 64 ? readlane_f64(a0, j) : readlane_f64(a1, j - 64);
+          const double xj = zj - aj * dv[q];
+          if (i0 == j) b0 = xj;
+          if (i1 == j) b1 = xj;
+          if (i0 < j) a0 += r0[q] * xj;
+          if (i1 < j) a1 += r1[q] * xj;
+        }
+      }
     }
-    if (i0 < n) x[i0] = b0;
-    if (i1 < n) x[i1] = b1;
+    if (v0) x[i0] = b0;
+    if (v1) x[i1] = b1;
   }
   __syncthreads();
 }
@@ -479,6 +546,10 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
   const Lds s = carve(lds_raw, n, H, ld);
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + b * a.ws_pp;
+#ifdef DRCVAR_MPC_STAMPS
+  unsigned long long stamp_acc[kStampSlots] = {};
+  unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   const int64_t pitch = static_cast<int64_t>(O) * kStepPad;
   const RowArrays rows{ws, ws + pitch, ws + 2 * pitch, ws + 3 * pitch,
                        ws + 4 * pitch, ws + 5 * pitch, ws + 6 * pitch, ws + 7 * pitch};
@@ -555,14 +626,17 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
   const double scale_q = 1.0 + fmax(fmaxv, kSlackLin);
   const double m_ineq = 2.0 * O * K + (a.has_u ? 2.0 * n : 0.0) + (a.has_p ? 4.0 * H : 0.0);
 
+  MPC_PHASE(0);
   int status = DRCVAR_MPC_STATUS_MAX_ITER;
   int it = 0, best_it = 0;
   double mu = 0.0, rp = 0.0, rd = 0.0, best_merit = kHuge;
   double* best_u = ws + kRowArrays * pitch;  // [n] best iterate
   for (it = 1; it <= a.max_iter; ++it) {
     // ---- positions of the iterate ----
+    MPC_PHASE(15);
     positions<NU>(s, s.u, s.p, s.c, H);
     __syncthreads();
+    MPC_PHASE(14);
 
     // ---- P1: residuals, weights, per-step S / v / affine rhs ----
     {
@@ -662,18 +736,23 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       if (best_merit < 1e-6 && it - best_it >= 8) break;  // stalled at the accuracy floor
     }
     const double gap = mu * m_ineq;
+    MPC_PHASE(1);
 
     // ---- K = H0 + diag(DU) + sum_k Mp' S_k Mp, affine rhs ----
     assemble_hessian<NU>(s, H0, n, ld, H);
     for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - gp_transpose<NU>(s, s.za, j, H);
     __syncthreads();
+    MPC_PHASE(2);
     if (!cholesky(s, n, ld)) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
+    MPC_PHASE(3);
     chol_solve(s, n, ld, s.dua);
+    MPC_PHASE(4);
     positions<NU>(s, s.dua, s.dpa, nullptr, H);
     __syncthreads();
+    MPC_PHASE(14);
 
     // ---- P2: affine step length ----
     double amax = kHuge;
@@ -779,9 +858,12 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       __syncthreads();
     }
     const double sigma_mu = s.sc[63];
+    MPC_PHASE(5);
     chol_solve(s, n, ld, s.du);
+    MPC_PHASE(4);
     positions<NU>(s, s.du, s.dp, nullptr, H);
     __syncthreads();
+    MPC_PHASE(14);
 
     // ---- P4: corrector step length ----
     amax = kHuge;
@@ -859,9 +941,11 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     __syncthreads();  // positions of the box loop read s.u; update it only after every reader
     for (int j = tid; j < n; j += kBlock) s.u[j] += alpha * s.du[j];
     __syncthreads();
+    MPC_PHASE(5);
   }
   if (it > a.max_iter) it = a.max_iter;
   __syncthreads();
+  MPC_PHASE(6);
   if (status != DRCVAR_MPC_STATUS_OPTIMAL && best_merit <= 1e3 * a.tol) {
     // stalled close to the optimum: return the best iterate, its slacks re-optimised below
     status = DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
@@ -949,7 +1033,9 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       }
       assemble_hessian<NU>(s, H0, n, ld, H);
       __syncthreads();
+      MPC_PHASE(10);
       if (!cholesky(s, n, ld)) break;
+      MPC_PHASE(11);
       for (int pass = 0; pass < kPolishIters; ++pass) {
         // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
         double acc[2] = {0, 0};
@@ -992,11 +1078,13 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
           s.du[j] = r;
         }
         __syncthreads();
+        MPC_PHASE(12);
         chol_solve(s, n, ld, s.du);
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
         positions<NU>(s, s.u, s.p, s.c, H);
         __syncthreads();
+        MPC_PHASE(13);
         // multiplier updates nu += rho * (E u - e)
         if (lane < K) {
           const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
@@ -1084,6 +1172,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     __syncthreads();
   }
 
+  MPC_PHASE(7);
   // ------------------------------- output -------------------------------
   const bool optimal = status == DRCVAR_MPC_STATUS_OPTIMAL || status == DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
   if (!optimal) {
@@ -1154,6 +1243,13 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     info[DRCVAR_MPC_INFO_POLISHED] = polished ? 1.0 : 0.0;
     info[DRCVAR_MPC_INFO_POLISH_ATTEMPTS] = polish_attempts;
   }
+  MPC_PHASE(8);
+#ifdef DRCVAR_MPC_STAMPS
+  if (tid == 0 && b < kStampProblems) {
+    stamp_acc[9] = it;
+    for (int k = 0; k < kStampSlots; ++k) g_mpc_stamps[b * kStampSlots + k] = stamp_acc[k];
+  }
+#endif
 }
 
 // ------------------------------- host side -------------------------------
@@ -1181,6 +1277,14 @@ int launch(const MpcArgs& args, int64_t n_problems, size_t lds_bytes, hipStream_
 }  // namespace
 
 extern "C" {
+
+#ifdef DRCVAR_MPC_STAMPS
+// diagnostic build only (not part of the ABI header)
+int drcvar_diag_mpc_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mpc_stamps), sizeof(g_mpc_stamps), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? kStampProblems : -1;
+}
+#endif
 
 int drcvar_mpc_model_init(const double* A, const double* B, const double* C, const double* Q,
                           const double* R, int32_t nx, int32_t nu, int32_t ny, int32_t H,

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase shader-clock totals of the MPC kernel from a -DDRCVAR_MPC_STAMPS build."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native  # noqa: E402
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf  # noqa: E402
+from mpc_bench import problem_batch  # noqa: E402
+
+NAMES = {0: "setup", 1: "P1 residuals+weights", 2: "assemble K", 3: "cholesky (ipm)",
+         4: "triangular solves (ipm)", 5: "row passes P2-P5", 6: "loop exit", 7: "polish other",
+         8: "output", 10: "polish classify+assemble", 11: "polish cholesky",
+         12: "polish row passes", 13: "polish solves", 14: "positions (ipm)", 15: "loop top"}
+dev = torch.device("cuda", 0)
+lib = _native.lib()
+lib.drcvar_diag_mpc_stamps.argtypes = [ctypes.c_void_p]
+for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
+    H, O, B = (int(v) for v in shape.split(","))
+    model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
+    x, u, info = mf.filter_batch(model, rec[..., 3:5], rec[..., 7], x0, xr, uf)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * (64 * 16))()
+    assert lib.drcvar_diag_mpc_stamps(ctypes.cast(buf, ctypes.c_void_p)) == 64
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(64, 16)[0].astype(np.int64)
+    tot = sum(st[k] for k in NAMES)
+    print(f"H={H} O={O}: total {tot} cycles ({tot / 100e6 * 1e3:.3f} ms at 100 MHz memtime), "
+          f"iterations {st[9]}, polish attempts {info[0, _native.MPC_INFO_POLISH_ATTEMPTS].item():.0f}")
+    for k, nm in NAMES.items():
+        print(f"  {nm:28s} {st[k]:10d} ({st[k] / tot * 100:5.1f}%)")
