@@ -140,6 +140,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true", help="skip the 2 GB roofline measurement")
+    ap.add_argument("--no-mpc", action="store_true", help="skip the MPC hand-off measurement")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path (several ranks may share one GPU)")
     args = ap.parse_args()
@@ -206,7 +207,7 @@ def main():
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed, kernel_s = float(t_max[0].item()), float(t_max[1].item())
 
-    large = None
+    large = mpc = None
     if rank == 0 and not args.no_large:
         Ol, Tl, Nl = LARGE
         s_l, e_l = synthetic.obstacle_batch(Ol, Tl, Nl, dev, seed=7)
@@ -225,6 +226,8 @@ def main():
                          load_traffic("c5"))
         large["workload"] = f"{Ol} obstacles x {Tl} steps x {Nl} samples (2.05 GB resident)"
         large["halfspaces_per_s"] = Ol * Tl / (large["kernel_ms"] * 1e-3)
+        if not args.no_mpc:
+            mpc = mpc_handoff(dev, s_l, e_l, params, with_cpu=world == 1 and not args.no_cpu_baseline)
         del s_l, e_l
         torch.cuda.empty_cache()
 
@@ -252,6 +255,7 @@ def main():
                        "alpha": params.alpha, "delta": params.delta, "epsilon": params.epsilon},
             "roofline": roofline(algorithmic_bytes(O, T, N), kernel_s, load_traffic(args.workload)),
             "roofline_large": large,
+            "mpc_handoff": mpc,
         }
         if world == 1 and not args.no_cpu_baseline:
             import numpy as np
@@ -269,6 +273,129 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def _mpc_problem_inputs(ego, H, B, dev):
+    """x0 / x_ref / fallback inputs of B problems following the ego straight line (main.py:74-89)."""
+    import numpy as np
+    e = ego.cpu().numpy()
+    xr = np.zeros((H + 1, 4))
+    xr[:min(H, len(e)), :2] = e[:H]
+    xr[min(H, len(e)):, :2] = e[min(H, len(e)) - 1]
+    xr[:-1, 2:] = (xr[1:, :2] - xr[:-1, :2]) / 0.2
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    return (T(np.repeat(xr[None, 0], B, 0)), T(np.repeat(xr[None], B, 0)),
+            T(np.zeros((B, H, 2))), xr)
+
+
+def mpc_handoff(dev, samples, ego, params, with_cpu):
+    """The QP hand-off (core/mpc_filter.py:40-178) measured two ways.
+
+    full_loop_c5: BASELINE config 5's "full MPC loop with QP handoff" on one GPU — the halfspace
+      kernel over the resident [256, 50, 10000] batch, then the DR-CVaR safety-filter QP over its
+      12 800 halfspaces (H = 50), both on the device, timed together with HIP events.
+    batched_reference: main.py's QP (multi_obstacle: 3 obstacles, H = 30, input bounds +-5,
+      position bounds +-10) for 1024 independent problems in one launch -> QPs/s; CPU baseline =
+      oracle/mpc_qp.py (sparse IPM + polish, 1 thread) on the same problem.
+    """
+    import numpy as np
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    dt = 0.2
+    A = np.block([[np.eye(2), dt * np.eye(2)], [np.zeros((2, 2)), np.eye(2)]])
+    Bm = np.block([[0.5 * dt ** 2 * np.eye(2)], [dt * np.eye(2)]])
+    C = np.block([np.eye(2), np.zeros((2, 2))])
+    Q, R = 2 * np.eye(4), np.eye(2)
+    ub = (np.full(2, -5.0), np.full(2, 5.0))
+    pb = (np.full(2, -10.0), np.full(2, 10.0))
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    out = {}
+    # ---- C5 full loop ----
+    O, T = samples.shape[0], samples.shape[1]
+    H = T
+    model = mf.MPCModel(A, Bm, C, Q, R, H, ub, pb, device=dev)
+    x0, xr, uf, xr_host = _mpc_problem_inputs(ego, H, 1, dev)
+    launch, rec = engine.prepare_safe_halfspaces(samples, ego, params)
+    h, g = mf.record_views(rec, "dr_cvar")
+    ws = torch.empty(model.workspace_doubles(1, O), dtype=torch.float64, device=dev)
+    res = {}
+
+    def qp():
+        res["x"], res["u"], res["info"] = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws)
+
+    def full():
+        launch()
+        qp()
+
+    full_ms = timed(full, 5)
+    qp_ms = timed(qp, 5)
+    info = res["info"][0].cpu().numpy()
+    c5 = {"workload": f"{O} obstacles x {T} steps x {samples.shape[2]} samples -> dr_cvar QP "
+                      f"(H={H}, {O * T} halfspace rows), 1 problem",
+          "full_step_ms": full_ms, "qp_ms": qp_ms, "halfspace_ms": full_ms - qp_ms,
+          "halfspace_constraints_per_s_full_loop": O * T / (full_ms * 1e-3),
+          "qp_status": mf.STATUS_NAMES.get(int(info[_native.MPC_INFO_STATUS])),
+          "qp_iterations": int(info[_native.MPC_INFO_ITERATIONS]),
+          "polished": bool(info[_native.MPC_INFO_POLISHED])}
+    if with_cpu:
+        from oracle import mpc_qp
+        r = rec.cpu().numpy()
+        hs = np.concatenate([r[..., 3:5], r[..., 7:8]], -1)
+        t0 = time.perf_counter()
+        xo, uo, io = mpc_qp.filter_trajectory(A, Bm, C, Q, R, H, xr_host[0], xr_host, None,
+                                              [hs[:, t] for t in range(T)], ub, pb)
+        c5["cpu_oracle_qp_s"] = time.perf_counter() - t0
+        c5["max_abs_err_u_vs_oracle"] = float(np.abs(res["u"][0].cpu().numpy() - uo).max())
+    out["full_loop_c5"] = c5
+    del ws, rec
+    # ---- batched reference configuration ----
+    Hr, Or, Bn = 30, 3, 1024
+    model_r = mf.MPCModel(A, Bm, C, Q, R, Hr, ub, pb, device=dev)
+    s_r, e_r = synthetic.obstacle_batch(Or, Hr, 20, dev, seed=3)       # NUM_SAMPLES = 20
+    rec_r = engine.safe_halfspaces(s_r, e_r, params)
+    hb = rec_r[None, :, :, 3:5].expand(Bn, Or, Hr, 2)
+    gb = rec_r[None, :, :, 7].expand(Bn, Or, Hr)
+    x0r, xrr, ufr, xr_host_r = _mpc_problem_inputs(e_r, Hr, Bn, dev)
+    wsr = torch.empty(model_r.workspace_doubles(Bn, Or), dtype=torch.float64, device=dev)
+
+    def qp_batch():
+        res["u"], res["info"] = mf.filter_batch(model_r, hb, gb, x0r, xrr, ufr, workspace=wsr)[1:]
+
+    ms = timed(qp_batch, 5)
+    inf = res["info"].cpu().numpy()
+    br = {"workload": f"main.py QP (H={Hr}, {Or} obstacles, bounds), {Bn} problems per launch",
+          "launch_ms": ms, "qps_per_s": Bn / (ms * 1e-3),
+          "optimal_frac": float((inf[:, _native.MPC_INFO_STATUS] == 0).mean()),
+          "mean_iterations": float(inf[:, _native.MPC_INFO_ITERATIONS].mean())}
+    if with_cpu:
+        from oracle import mpc_qp
+        r = rec_r.cpu().numpy()
+        hs = np.concatenate([r[..., 3:5], r[..., 7:8]], -1)
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            xo, uo, io = mpc_qp.filter_trajectory(A, Bm, C, Q, R, Hr, xr_host_r[0], xr_host_r, None,
+                                                  [hs[:, t] for t in range(Hr)], ub, pb)
+            reps += 1
+        el = time.perf_counter() - t0
+        br["cpu_baseline"] = {"value": reps / el, "unit": "QPs/s", "cores": 1, "kind": "port",
+                              "sample": f"{reps} solves of problem 0 by oracle/mpc_qp.py ({el:.1f} s)"}
+        br["max_abs_err_u_vs_oracle"] = float(np.abs(res["u"][0].cpu().numpy() - uo).max())
+    out["batched_reference"] = br
+    out["bound"] = ("latency: one workgroup per problem runs the whole interior-point solve "
+                    "(dense LDL' + triangular solves in LDS dominate; see DESIGN.md)")
+    return out
 
 
 def _cpu_model():
