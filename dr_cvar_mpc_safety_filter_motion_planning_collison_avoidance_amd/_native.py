@@ -18,9 +18,11 @@ LIB_PATH = os.path.join(LIB_DIR, "libdrcvar_halfspace.so")
 # diagnostic builds only (scripts/diag_stages.sh); the product always loads LIB_PATH
 LIB_PATH = os.environ.get("DRCVAR_DIAG_LIB", LIB_PATH)
 SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip"),
-           os.path.join(PKG_DIR, "csrc", "drcvar_mpc.hip")]
+           os.path.join(PKG_DIR, "csrc", "drcvar_mpc.hip"),
+           os.path.join(PKG_DIR, "csrc", "drcvar_sampling.hip")]
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
-HEADERS = [os.path.join(INCLUDE_DIR, "drcvar_halfspace.h"), os.path.join(INCLUDE_DIR, "drcvar_mpc.h")]
+HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("drcvar_halfspace.h", "drcvar_mpc.h",
+                                                  "drcvar_sampling.h")]
 OFFLOAD_ARCH = os.environ.get("DRCVAR_OFFLOAD_ARCH", "gfx950")
 
 ABI_VERSION = 1
@@ -62,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "drcvar_mpc_model_init",
     "drcvar_mpc_workspace_doubles",
     "drcvar_mpc_filter_f64",
+    "drcvar_sample_trajectories_f64",
 )
 
 
@@ -121,6 +124,10 @@ def _bind(lib):
         modelp, ptr, i64, ptr, ptr, i64, i64, i64, i64, i64, i64, i64, i64, ptr, i64, ptr, i64,
         i64, ptr, i64, i64, i32, dbl, i32, ptr, ptr, ptr, ptr, i64, ptr]
     lib.drcvar_mpc_filter_f64.restype = ctypes.c_int
+    u64 = ctypes.c_uint64
+    lib.drcvar_sample_trajectories_f64.argtypes = [
+        ptr, i64, i64, i64, i64, i64, dbl, dbl, dbl, u64, u64, i32, ptr, i64, i64, i64, ptr]
+    lib.drcvar_sample_trajectories_f64.restype = ctypes.c_int
     return lib
 
 

@@ -76,7 +76,9 @@ class SafetyFilteringEnvironment:
             # [G, N, n_steps, 2] slice of the reference layout, staged as-is (environment.py:88)
             host = np.stack([np.asarray(obstacle_sample_trajectories[i], dtype=np.float64)[:, :n_steps, :]
                              for i in idx])
-            dev_s = torch.as_tensor(host).to(dev)
+            # one pinned staging copy, asynchronous H2D; the kernel reads the reference's
+            # [G, N, T, 2] order through strides (no transpose pass)
+            dev_s = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
             view = dev_s.permute(0, 2, 1, 3)                                  # [G, T, N, 2] strided
             launches.append((idx, view))
         t1 = time.time()

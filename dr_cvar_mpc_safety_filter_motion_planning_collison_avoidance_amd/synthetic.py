@@ -7,13 +7,16 @@ obstacle o moves on a straight line from a start ~ U[-5, 5]^2 with heading ~ U[0
 N(0, diag(0.01, 0.01)) noise (``simulation/obstacles.py:62-74``, cov at :134), noise-free at t = 0
 (:63).  The ego follows the straight line (-4, 0) -> (4, 0) at 1.5 m/s
 (``simulation/planner.py:120-197``).  Output is the packed ``[O, T, N, 2]`` float64 layout the
-kernel streams at full coalescing, and ego ``[T, 2]``.
+kernel streams at full coalescing, and ego ``[T, 2]``.  The samples are drawn by the device
+sampler (``drcvar_sample_trajectories_f64``, Philox4x32-10), so nothing is staged from the host.
 """
 from __future__ import annotations
 
 import math
 
 import torch
+
+from .simulation.obstacles import sample_trajectories_device
 
 DT = 0.2
 NOISE_STD = 0.1  # sqrt(0.01)
@@ -43,10 +46,7 @@ def obstacle_batch(n_obstacles: int, n_steps: int, n_samples: int, device, seed:
     speed = 0.6 + torch.rand((n_obstacles,), generator=g, **f64) * 0.9
     vel = torch.stack([torch.cos(heading), torch.sin(heading)], dim=1) * speed[:, None]
     t = torch.arange(n_steps, **f64) * DT
-    nominal = start[:, None, :] + t[None, :, None] * vel[:, None, :]          # [O, T, 2]
-    samples = torch.randn((n_obstacles, n_steps, n_samples, 2), generator=g, **f64)
-    samples.mul_(NOISE_STD)
-    if n_steps > 0:
-        samples[:, 0].zero_()                                                  # obstacles.py:63
-    samples.add_(nominal[:, :, None, :])
+    nominal = (start[:, None, :] + t[None, :, None] * vel[:, None, :]).contiguous()   # [O, T, 2]
+    samples = sample_trajectories_device(nominal, n_samples, [[NOISE_STD ** 2, 0.0], [0.0, NOISE_STD ** 2]],
+                                         seed=seed, zero_first_step=True)             # obstacles.py:63
     return samples, straight_line_ego(n_steps, device)

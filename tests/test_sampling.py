@@ -1,0 +1,117 @@
+"""Obstacle sample generation: simulation/obstacles.py, host and device.
+
+CPU: the host mirror reproduces the reference's RNG stream bit for bit (the golden vectors were
+drawn by the reference's own generate_obstacle_scenarios with seed 42) and the layout packer is
+a pure transpose.  GPU: the Philox sampler's distribution (moments, correlation, normality),
+determinism and stream separation, the noise-free first step, strided outputs, and the
+sampler -> halfspace kernel pipeline against the C oracle on the same samples.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DIR, OFFSET_TOL, load_golden
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.config.scenarios import get_scenario_config
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.simulation import obstacles as ob
+
+
+@pytest.mark.parametrize("name,scenario,n,keep", [("head_on_n100_t20", "head_on", 100, 20),
+                                                  ("multi_obstacle_n1000_t8", "multi_obstacle", 1000, 8),
+                                                  ("multi_obstacle_n20_h30", "multi_obstacle", 20, 30)])
+def test_host_generator_reproduces_reference_stream(name, scenario, n, keep):
+    gold = load_golden(os.path.join(GOLDEN_DIR, f"{name}.npz"))
+    np.random.seed(42)                                            # main.py:191
+    data = ob.generate_obstacle_scenarios(get_scenario_config(scenario), 30.0, 0.2, n)
+    got = np.stack([np.transpose(tr[:, :keep], (1, 0, 2)) for tr in data["sample_trajectories"]])
+    np.testing.assert_array_equal(got, gold["samples"])
+    assert len(data["realization_trajectories"]) == got.shape[0]
+    for nom, real in zip(data["nominal_trajectories"], data["realization_trajectories"]):
+        assert nom.shape == (151, 2) and real.shape == (151, 2)
+        np.testing.assert_array_equal(real[0], nom[0])
+
+
+def test_nominal_trajectory_rules():
+    p = ob.generate_nominal_trajectory(np.array([1.0, 2.0]), np.array([0.0, 0.0]), 1.0, 5, 0.2)
+    np.testing.assert_array_equal(p, np.tile([1.0, 2.0], (6, 1)))        # stationary (:23-25)
+    p = ob.generate_nominal_trajectory(np.array([0.0, 0.0]), np.array([3.0, 4.0]), 2.0, 3, 0.5)
+    np.testing.assert_allclose(p[-1], [3 * 0.5 * 2.0 * 0.6, 3 * 0.5 * 2.0 * 0.8], atol=1e-15)
+
+
+def test_pack_layout_is_a_transpose():
+    import torch
+    rng = np.random.default_rng(0)
+    trs = [rng.normal(size=(7, 11, 2)) for _ in range(3)]
+    packed = ob.pack_sample_trajectories(trs, 9, torch.device("cpu"), pin=False)
+    assert tuple(packed.shape) == (3, 9, 7, 2) and packed.is_contiguous()
+    np.testing.assert_array_equal(packed.numpy(), np.stack([np.transpose(t[:, :9], (1, 0, 2)) for t in trs]))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _nominal(dev, O=2, T=3):
+    import torch
+    nom = torch.tensor([[[0.5 * o + 0.1 * t, -0.25 * o + 0.2 * t] for t in range(T)] for o in range(O)],
+                       dtype=torch.float64)
+    return nom.to(dev)
+
+
+@pytest.mark.gpu
+def test_device_sampler_moments_and_normality(dev):
+    from scipy import stats
+    nom = _nominal(dev)
+    N = 400_000
+    for cov in (ob.NOISE_COV, np.array([[0.04, 0.012], [0.012, 0.02]])):
+        s = ob.sample_trajectories_device(nom, N, cov, seed=123).cpu().numpy()
+        nh = nom.cpu().numpy()
+        np.testing.assert_array_equal(s[:, 0], np.broadcast_to(nh[:, 0, None, :], s[:, 0].shape))
+        L = np.linalg.cholesky(cov)
+        for o in range(s.shape[0]):
+            for t in range(1, s.shape[1]):
+                d = s[o, t] - nh[o, t]
+                se = np.sqrt(np.diag(cov) / N)
+                assert np.all(np.abs(d.mean(0)) < 5 * se), (o, t, d.mean(0))
+                emp = np.cov(d.T)
+                assert np.all(np.abs(emp - cov) < 6 * np.sqrt(2.0 / N) * np.max(cov)), emp
+                z = np.linalg.solve(L, d.T)
+                for comp in z:
+                    assert stats.kstest(comp, "norm").pvalue > 1e-4
+
+
+@pytest.mark.gpu
+def test_device_sampler_determinism_streams_and_strides(dev):
+    import torch
+    nom = _nominal(dev, 3, 4)
+    a = ob.sample_trajectories_device(nom, 1000, seed=7)
+    b = ob.sample_trajectories_device(nom, 1000, seed=7)
+    assert torch.equal(a, b)
+    c = ob.sample_trajectories_device(nom, 1000, seed=8)
+    d = ob.sample_trajectories_device(nom, 1000, seed=7, stream_offset=1)
+    assert not torch.equal(a[:, 1:], c[:, 1:]) and not torch.equal(a[:, 1:], d[:, 1:])
+    # a strided destination (the reference's [O, N, T, 2] order) receives the same values
+    big = torch.zeros((3, 1000, 4, 2), dtype=torch.float64, device=dev)
+    ob.sample_trajectories_device(nom, 1000, seed=7, out=big.permute(0, 2, 1, 3))
+    assert torch.equal(big.permute(0, 2, 1, 3), a)
+    # the noise-free first step is optional
+    e = ob.sample_trajectories_device(nom, 1000, seed=7, zero_first_step=False)
+    assert torch.equal(e[:, 1:], a[:, 1:]) and not torch.equal(e[:, 0], a[:, 0])
+
+
+@pytest.mark.gpu
+def test_device_scenario_feeds_the_engine(dev):
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import engine, synthetic
+    from oracle import c_oracle
+    data = ob.generate_obstacle_scenarios_device(get_scenario_config("multi_obstacle"), 30.0, 0.2,
+                                                 1000, seed=5, device=dev)
+    samples = data["sample_trajectories"][:, :20]                  # [O, 20, N, 2] view
+    ego = synthetic.straight_line_ego(20, dev, start=(-2.0, -1.0), goal=(4.0, 0.0))
+    rec = engine.safe_halfspaces(samples, ego, engine.RiskParams()).cpu().numpy()
+    ref = c_oracle.safe_halfspaces(samples.contiguous().cpu().numpy(), ego.cpu().numpy(),
+                                   0.3, 0.3, 0.2, 0.1, 0.15)
+    assert np.max(np.abs(rec - ref)) < OFFSET_TOL
