@@ -207,7 +207,7 @@ def main():
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed, kernel_s = float(t_max[0].item()), float(t_max[1].item())
 
-    large = mpc = None
+    large = mpc = sampling = None
     if rank == 0 and not args.no_large:
         Ol, Tl, Nl = LARGE
         s_l, e_l = synthetic.obstacle_batch(Ol, Tl, Nl, dev, seed=7)
@@ -226,6 +226,7 @@ def main():
                          load_traffic("c5"))
         large["workload"] = f"{Ol} obstacles x {Tl} steps x {Nl} samples (2.05 GB resident)"
         large["halfspaces_per_s"] = Ol * Tl / (large["kernel_ms"] * 1e-3)
+        sampling = sampler_roofline(s_l, stream)
         if not args.no_mpc:
             mpc = mpc_handoff(dev, s_l, e_l, params, with_cpu=world == 1 and not args.no_cpu_baseline)
         del s_l, e_l
@@ -256,6 +257,7 @@ def main():
             "roofline": roofline(algorithmic_bytes(O, T, N), kernel_s, load_traffic(args.workload)),
             "roofline_large": large,
             "mpc_handoff": mpc,
+            "sampling": sampling,
         }
         if world == 1 and not args.no_cpu_baseline:
             import numpy as np
@@ -273,6 +275,28 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def sampler_roofline(out, stream, reps=10):
+    """Device sample generator (drcvar_sample_trajectories_f64) refilling a resident batch: bytes
+    written (16 per sample) per launch / event time -- an HBM-write-bound kernel."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.simulation import obstacles
+    O, T, N, _ = out.shape
+    nominal = out[:, :, 0, :].clone()                    # any [O, T, 2] nominal path
+    launch = lambda: obstacles.sample_trajectories_device(nominal, N, seed=11, out=out)
+    launch()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(reps):
+        launch()
+    b.record(stream)
+    torch.cuda.synchronize()
+    sec = a.elapsed_time(b) * 1e-3 / reps
+    written = O * T * N * 16
+    return {"workload": f"{O}x{T}x{N} samples (Philox4x32-10 + Box-Muller, fp64)", "kernel_ms": sec * 1e3,
+            "samples_per_s": O * T * N / sec, "bound": "hbm", "achieved": written / sec / 1e9,
+            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": written / sec / HBM_PEAK}
 
 
 def _mpc_problem_inputs(ego, H, B, dev):
