@@ -46,6 +46,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
 constexpr int kRowArrays = 8; // h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
 constexpr int kBestPad = 128; // best iterate u (n <= DRCVAR_MPC_MAX_DECISION)
+constexpr int kRowStride = kRowArrays * kStepPad;  // one obstacle's block of the workspace
 constexpr double kSlackLin = 50.0;    // core/mpc_filter.py:143
 constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:144
 constexpr double kStepFrac = 0.995;
@@ -99,7 +100,7 @@ BlobLayout blob_layout(int nx, int nu, int H) {
 struct MpcArgs {
   const double* blob;
   BlobLayout off;
-  int nx, nu, H, n, K, O, ld;
+  int nx, nu, H, n, K, O;
   int has_u, has_p;
   double umin[DRCVAR_MPC_MAX_INPUTS], umax[DRCVAR_MPC_MAX_INPUTS], pmin[2], pmax[2];
   const double* hs_h;
@@ -121,7 +122,7 @@ struct MpcArgs {
   int polish;
 };
 
-// LDS carve (doubles), sized from (n, H, ld) only; lds_doubles() and carve() must agree.
+// LDS arrays (doubles); offsets from LdsPlan below.
 struct Lds {
   double* K;      // [n][ld] lower triangle, overwritten by the Cholesky factor
   double* diag;   // [n] pivots L_jj
@@ -149,39 +150,70 @@ struct Lds {
   double* sc;     // [64] block scalars
 };
 
-inline int64_t lds_doubles(int n, int H, int ld) {
-  return static_cast<int64_t>(n) * ld + 13LL * n + 14LL * H + 8LL * H + 3LL * H +
-         2LL * DRCVAR_MPC_MAX_INPUTS * H + static_cast<int64_t>(H + 1) * DRCVAR_MPC_MAX_STATES +
-         static_cast<int64_t>(kWaves) * kPerStepQ * 64 + 64;
-}
+// Fixed LDS plan per size class: every array sits at a compile-time offset, so LDS addresses are
+// immediates and no scalar registers hold array bases.  NMAX = 64 (n <= 64, any H <= 64) or
+// NMAX = 120 (n in 65..120; then nu >= 2, so H <= 60).
+template <int NMAX>
+struct LdsPlan {
+  static constexpr int HM = NMAX <= 64 ? DRCVAR_MPC_MAX_HORIZON : 60;
+  static constexpr int ld = NMAX + 1;  // odd: column walks hit distinct banks
+  static constexpr int K = 0;
+  static constexpr int diag = K + NMAX * ld;
+  static constexpr int u = diag + NMAX;
+  static constexpr int dua = u + NMAX;
+  static constexpr int du = dua + NMAX;
+  static constexpr int rdu = du + NMAX;
+  static constexpr int f = rdu + NMAX;
+  static constexpr int DU = f + NMAX;
+  static constexpr int rU = DU + NMAX;
+  static constexpr int rUu = rU + NMAX;
+  static constexpr int bx = rUu + NMAX;
+  static constexpr int c = bx + 4 * NMAX;
+  static constexpr int p = c + 2 * HM;
+  static constexpr int dpa = p + 2 * HM;
+  static constexpr int dp = dpa + 2 * HM;
+  static constexpr int v = dp + 2 * HM;
+  static constexpr int za = v + 2 * HM;
+  static constexpr int zu = za + 2 * HM;
+  static constexpr int px = zu + 2 * HM;
+  static constexpr int S = px + 8 * HM;
+  static constexpr int Mp = S + 3 * HM;
+  static constexpr int xs = Mp + 2 * DRCVAR_MPC_MAX_INPUTS * HM;
+  static constexpr int red = xs + (HM + 1) * DRCVAR_MPC_MAX_STATES;
+  static constexpr int sc = red + kWaves * kPerStepQ * 64;
+  static constexpr int total = sc + 64;
+};
+static_assert(LdsPlan<120>::total * 8 <= 160 * 1024, "LDS plan exceeds 160 KB");
+static_assert(LdsPlan<64>::total * 8 <= 80 * 1024, "small plan should allow two workgroups per CU");
 
-__device__ inline Lds carve(double* base, int n, int H, int ld) {
+template <int NMAX>
+__device__ inline Lds carve(double* base) {
+  using P = LdsPlan<NMAX>;
   Lds s;
-  double* q = base;
-  s.K = q; q += static_cast<int64_t>(n) * ld;
-  s.diag = q; q += n;
-  s.u = q; q += n;
-  s.dua = q; q += n;
-  s.du = q; q += n;
-  s.rdu = q; q += n;
-  s.f = q; q += n;
-  s.DU = q; q += n;
-  s.rU = q; q += n;
-  s.rUu = q; q += n;
-  s.bx = q; q += 4 * n;
-  s.c = q; q += 2 * H;
-  s.p = q; q += 2 * H;
-  s.dpa = q; q += 2 * H;
-  s.dp = q; q += 2 * H;
-  s.v = q; q += 2 * H;
-  s.za = q; q += 2 * H;
-  s.zu = q; q += 2 * H;
-  s.px = q; q += 8 * H;
-  s.S = q; q += 3 * H;
-  s.Mp = q; q += 2 * DRCVAR_MPC_MAX_INPUTS * H;
-  s.xs = q; q += (H + 1) * DRCVAR_MPC_MAX_STATES;
-  s.red = q; q += kWaves * kPerStepQ * 64;
-  s.sc = q;
+  s.K = base + P::K;
+  s.diag = base + P::diag;
+  s.u = base + P::u;
+  s.dua = base + P::dua;
+  s.du = base + P::du;
+  s.rdu = base + P::rdu;
+  s.f = base + P::f;
+  s.DU = base + P::DU;
+  s.rU = base + P::rU;
+  s.rUu = base + P::rUu;
+  s.bx = base + P::bx;
+  s.c = base + P::c;
+  s.p = base + P::p;
+  s.dpa = base + P::dpa;
+  s.dp = base + P::dp;
+  s.v = base + P::v;
+  s.za = base + P::za;
+  s.zu = base + P::zu;
+  s.px = base + P::px;
+  s.S = base + P::S;
+  s.Mp = base + P::Mp;
+  s.xs = base + P::xs;
+  s.red = base + P::red;
+  s.sc = base + P::sc;
   return s;
 }
 
@@ -256,7 +288,17 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double ratio(double x, double dx) { return dx < 0.0 ? -x / dx : kHuge; }
+// 1/x from the hardware estimate plus one Newton step (~1 ulp; the IEEE division sequence is
+// ~10 dependent instructions and the row passes perform a dozen per halfspace row)
+__device__ __forceinline__ double rcp(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+// step-to-boundary ratio; only feeds the 0.995 fraction of the step length, so the raw estimate
+__device__ __forceinline__ double ratio(double x, double dx) {
+  return dx < 0.0 ? -x * __builtin_amdgcn_rcp(dx) : kHuge;
+}
 
 // p[2k+i] = c[2k+i] + sum_{j<=k} Mp[k-j][i][:] . u[j*nu : (j+1)*nu]
 template <int NU>
@@ -322,108 +364,166 @@ __device__ inline void assemble_hessian(const Lds& s, const double* H0, int n, i
   }
 }
 
-// Right-looking LDL' factorisation of the lower triangle of K (n x n, leading dimension ld), in
-// place, with UNSCALED columns: afterwards K[i][j] (i > j) = L_ij d_j and s.diag[j] = 1 / d_j.
-// Keeping the columns unscaled lets step j read column j while the trailing update writes only
-// columns > j, so each column costs ONE barrier.  Two threads per trailing column (even / odd
-// rows); each thread issues its loads in groups of four before the dependent stores, so the LDS
-// latency is paid once per group.  Returns false on a non-positive or non-finite pivot (uniform).
+// Right-looking LDL' factorisation of the lower triangle of K (n x n, leading dimension ld) with
+// UNSCALED columns: afterwards K[i][j] (i > j) = L_ij d_j and s.diag[j] = 1 / d_j.
+// The matrix lives in REGISTERS during the factorisation: thread (tr, tc) of a 16 x 16 grid owns
+// the elements K[tr + 16a][tc + 16b] (a, b < 8, so n <= 128), 64 doubles, statically indexed.
+// Columns are processed in blocks of 16 (jb runtime, jr = j mod 16 unrolled): at the start of a
+// block each thread copies its column jb into `cur` (one select chain per block, not per step)
+// and keeps it updated alongside the tile, so the owners of column j (tc == jr) publish it with
+// static indices.  The column goes through an LDS buffer double-buffered by parity: one barrier
+// per column.  Row groups a whose rows are all above the trailing part are skipped (the test is
+// uniform across a wave except within one 4-row window).  The factor is written back to LDS for
+// the solves.  Returns false on a non-positive or non-finite pivot (uniform).
+constexpr int kTile = 16;
+
+template <int kOwn>
 __device__ inline bool cholesky(const Lds& s, int n, int ld) {
-  const int tid = threadIdx.x;
+  static_assert(kBlock == kTile * kTile && kOwn <= 8, "tile grid");
+  const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
   double* K = s.K;
-  const int col_off = tid & 127, half = tid >> 7;
-  static_assert(kBlock == 256 && DRCVAR_MPC_MAX_DECISION <= 128, "two threads per column");
-  for (int j = 0; j < n; ++j) {
-    const double d = K[j * ld + j];
-    if (!(d > 0.0) || !isfinite(d)) return false;
-    const double invd = 1.0 / d;
-    if (tid == 0) s.diag[j] = invd;
-    const int k = j + 1 + col_off;
-    if (k < n) {
-      const double lkj = K[k * ld + j] * invd;
-      int i = k + half;
-      for (; i + 6 < n; i += 8) {
-        double a[4], c[4];
+  double* col = s.red;  // [2][128 + 1] column buffers, pivot in slot 128
+  double v[kOwn][kOwn];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          a[q] = K[(i + 2 * q) * ld + j];
-          c[q] = K[(i + 2 * q) * ld + k];
-        }
+  for (int a = 0; a < kOwn; ++a)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) K[(i + 2 * q) * ld + k] = c[q] - a[q] * lkj;
-      }
-      for (; i < n; i += 2) K[i * ld + k] -= K[i * ld + j] * lkj;
+    for (int b = 0; b < kOwn; ++b) {
+      const int i = tr + kTile * a, k = tc + kTile * b;
+      v[a][b] = (i < n && k <= i) ? K[i * ld + k] : 0.0;
     }
-    __syncthreads();
+  const int nblk = (n + kTile - 1) / kTile;
+  for (int jb = 0; jb < nblk; ++jb) {
+    double cur[kOwn];
+#pragma unroll
+    for (int a = 0; a < kOwn; ++a) {
+      double val = 0.0;
+#pragma unroll
+      for (int b = 0; b < kOwn; ++b) val = b == jb ? v[a][b] : val;
+      cur[a] = val;
+    }
+#pragma unroll
+    for (int jr = 0; jr < kTile; ++jr) {
+      const int j = jb * kTile + jr;
+      if (j >= n) break;
+      double* buf = col + (jr & 1) * 129;
+      if (tc == jr) {
+#pragma unroll
+        for (int a = 0; a < kOwn; ++a) {
+          const int i = tr + kTile * a;
+          buf[i] = i > j ? cur[a] : 0.0;
+          if (i == j) buf[128] = cur[a];
+        }
+      }
+      __syncthreads();
+      // every LDS operand of the step in one round trip
+      const double d = buf[128];
+      const double cj = buf[tc + kTile * jb];
+      double ck[kOwn], ci[kOwn];
+#pragma unroll
+      for (int b = 0; b < kOwn; ++b) ck[b] = buf[tc + kTile * b];
+#pragma unroll
+      for (int a = 0; a < kOwn; ++a) ci[a] = buf[tr + kTile * a];
+      if (!(d > 0.0) || !isfinite(d)) return false;  // uniform
+      const double invd = 1.0 / d;
+      if (tid == 0) s.diag[j] = invd;
+#pragma unroll
+      for (int b = 0; b < kOwn; ++b) ck[b] *= invd;
+      const double cjs = cj * invd;
+#pragma unroll
+      for (int a = 0; a < kOwn; ++a) {
+        if (tr + kTile * a > j) {
+#pragma unroll
+          for (int b = 0; b < kOwn; ++b) v[a][b] -= ci[a] * ck[b];
+          cur[a] -= ci[a] * cjs;
+        }
+      }
+    }
   }
+#pragma unroll
+  for (int a = 0; a < kOwn; ++a)
+#pragma unroll
+    for (int b = 0; b < kOwn; ++b) {
+      const int i = tr + kTile * a, k = tc + kTile * b;
+      if (i < n && k <= i) K[i * ld + k] = v[a][b];
+    }
+  __syncthreads();
   return true;
 }
 
-// Solve K x = b with the factor above, b in x[0..n) (LDS), by wave 0; rows lane and lane + 64
-// live in registers and the pivot value travels by readlane.  The LDS operands are loaded eight
-// steps at a time, so the LDS latency is paid once per eight steps and the dependent chain per
-// step is readlane -> mul -> fma.
-constexpr int kSolveBlock = 8;
-
+// Solve K x = b with the factor above, b in x[0..n) (LDS).  Blocked by 16: the diagonal block is
+// solved by wave 0 (lane = row, pivots by readlane, the block's 16 factor entries of each lane
+// loaded up front), the rows below / above are updated by all threads with a 16-wide dot
+// product each.  Forward: z_j = b_j / d_j, b_i -= C_ij z_j.  Backward: x_j = z_j -
+// (sum_{i>j} C_ij x_i) / d_j.
 __device__ inline void chol_solve(const Lds& s, int n, int ld, double* x) {
   const int tid = threadIdx.x;
-  if (tid < 64) {
-    const double* K = s.K;
-    const int i0 = tid, i1 = tid + 64;
-    const bool v0 = i0 < n, v1 = i1 < n;
-    double b0 = v0 ? x[i0] : 0.0;
-    double b1 = v1 ? x[i1] : 0.0;
-    // forward: z_j = b_j / d_j, b_i -= C_ij z_j  (C = L D, unit-lower L)
-    for (int jb = 0; jb < n; jb += kSolveBlock) {
-      double c0[kSolveBlock], c1[kSolveBlock], dv[kSolveBlock];
+  const double* K = s.K;
+  const int nb = (n + kTile - 1) / kTile;
+  for (int J = 0; J < nb; ++J) {
+    const int j0 = J * kTile, j1 = min(j0 + kTile, n);
+    if (tid < 64) {
+      const int i = j0 + tid;
+      const bool mine = tid < kTile && i < j1;
+      double c[kTile], dv[kTile];
 #pragma unroll
-      for (int q = 0; q < kSolveBlock; ++q) {
-        const int j = jb + q < n ? jb + q : n - 1;
-        c0[q] = v0 ? K[i0 * ld + j] : 0.0;
-        c1[q] = v1 ? K[i1 * ld + j] : 0.0;
+      for (int q = 0; q < kTile; ++q) {
+        const int j = min(j0 + q, n - 1);
+        c[q] = (mine && i > j) ? K[i * ld + j] : 0.0;
         dv[q] = s.diag[j];
       }
+      double bi = mine ? x[i] : 0.0;
 #pragma unroll
-      for (int q = 0; q < kSolveBlock; ++q) {
-        const int j = jb + q;
-        if (j < n) {
-          const double zj = (j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64)) * dv[q];
-          if (i0 == j) b0 = zj;
-          if (i1 == j) b1 = zj;
-          if (i0 > j) b0 -= c0[q] * zj;
-          if (i1 > j) b1 -= c1[q] * zj;
+      for (int q = 0; q < kTile; ++q) {
+        if (j0 + q < j1) {
+          const double zj = readlane_f64(bi, q) * dv[q];
+          bi = tid == q ? zj : bi - c[q] * zj;
         }
       }
+      if (mine) x[i] = bi;
     }
-    // backward: x_j = z_j - (sum_{i>j} C_ij x_i) / d_j, accumulated row by row
-    double a0 = 0.0, a1 = 0.0;
-    for (int jt = n - 1; jt >= 0; jt -= kSolveBlock) {
-      double r0[kSolveBlock], r1[kSolveBlock], dv[kSolveBlock];
-#pragma unroll
-      for (int q = 0; q < kSolveBlock; ++q) {
-        const int j = jt - q >= 0 ? jt - q : 0;
-        r0[q] = i0 < j ? K[j * ld + i0] : 0.0;
-        r1[q] = i1 < j ? K[j * ld + i1] : 0.0;
-        dv[q] = s.diag[j];
-      }
-#pragma unroll
-      for (int q = 0; q < kSolveBlock; ++q) {
-        const int j = jt - q;
-        if (j >= 0) {
-          const double zj = j < 64 ? readlane_f64(b0, j) : readlane_f64(b1, j - 64);
-          const double aj = j < 64 ? readlane_f64(a0, j) : readlane_f64(a1, j - 64);
-          const double xj = zj - aj * dv[q];
-          if (i0 == j) b0 = xj;
-          if (i1 == j) b1 = xj;
-          if (i0 < j) a0 += r0[q] * xj;
-          if (i1 < j) a1 += r1[q] * xj;
-        }
-      }
+    __syncthreads();
+    for (int i = j1 + tid; i < n; i += kBlock) {
+      double acc = x[i];
+#pragma unroll 4
+      for (int j = j0; j < j1; ++j) acc -= K[i * ld + j] * x[j];
+      x[i] = acc;
     }
-    if (v0) x[i0] = b0;
-    if (v1) x[i1] = b1;
+    __syncthreads();
   }
-  __syncthreads();
+  for (int J = nb - 1; J >= 0; --J) {
+    const int j0 = J * kTile, j1 = min(j0 + kTile, n);
+    if (tid < 64) {
+      const int i = j0 + tid;
+      const bool mine = tid < kTile && i < j1;
+      double r[kTile], dv[kTile];
+#pragma unroll
+      for (int q = 0; q < kTile; ++q) {
+        const int j = min(j0 + q, n - 1);
+        r[q] = (mine && i < j) ? K[j * ld + i] : 0.0;
+        dv[q] = s.diag[j];
+      }
+      // x[i] holds z_i minus the later blocks' contributions (already divided by d_i)
+      double xi = mine ? x[i] : 0.0;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = kTile - 1; q >= 0; --q) {
+        if (j0 + q < j1) {
+          const double xj = readlane_f64(xi, q) - readlane_f64(acc, q) * dv[q];
+          if (tid == q) xi = xj;
+          acc += r[q] * xj;
+        }
+      }
+      if (mine) x[i] = xi;
+    }
+    __syncthreads();
+    for (int rr = tid; rr < j0; rr += kBlock) {
+      double acc = 0.0;
+#pragma unroll 4
+      for (int j = j0; j < j1; ++j) acc += K[j * ld + rr] * x[j];
+      x[rr] -= acc * s.diag[rr];
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -436,7 +536,7 @@ struct HsRow {
   double h0, h1, g, sv, wA, lA, wB, lB;
 };
 struct HsLin {
-  double rpA, rpB, rds, DA, DB, sig;
+  double rpA, rpB, rds, DA, DB, sig, iwA, iwB, isig;
 };
 struct RowDir {
   double ds, dwA, dlA, dwB, dlB;
@@ -447,18 +547,21 @@ __device__ __forceinline__ HsLin hs_lin(const HsRow& q, double p0, double p1) {
   l.rpA = q.h0 * p0 + q.h1 * p1 + q.g - q.sv + q.wA;  // h.p + g - s + w_hs
   l.rpB = q.wB - q.sv;                                // -s + w_s
   l.rds = kSlackHess * q.sv + kSlackLin - q.lA - q.lB;
-  l.DA = q.lA / q.wA;
-  l.DB = q.lB / q.wB;
+  l.iwA = rcp(q.wA);
+  l.iwB = rcp(q.wB);
+  l.DA = q.lA * l.iwA;
+  l.DB = q.lB * l.iwB;
   l.sig = kSlackHess + l.DA + l.DB;
+  l.isig = rcp(l.sig);
   return l;
 }
 
 // Slack eliminated per row: ds = (rhs_s + D_A h.dp) / sig with rhs_s = -r_ds + rho_A + rho_B.
 __device__ __forceinline__ RowDir hs_dir(const HsLin& l, double rhoA, double rhoB, double hdp) {
   RowDir d;
-  d.ds = (-l.rds + rhoA + rhoB + l.DA * hdp) / l.sig;
+  d.ds = (-l.rds + rhoA + rhoB + l.DA * hdp) * l.isig;
   // gA = h.dp - ds written without the cancellation of two ~D_A-sized terms
-  const double gA = (hdp * (kSlackHess + l.DB) + l.rds - rhoA - rhoB) / l.sig;
+  const double gA = (hdp * (kSlackHess + l.DB) + l.rds - rhoA - rhoB) * l.isig;
   d.dwA = -l.rpA - gA;
   d.dlA = l.DA * gA + rhoA;
   d.dwB = -l.rpB + d.ds;
@@ -473,8 +576,8 @@ __device__ __forceinline__ RowDir hs_affine(const HsRow& q, const HsLin& l, doub
 __device__ __forceinline__ RowDir hs_corrector(const HsRow& q, const HsLin& l, double hdpa,
                                                double hdp, double sigma_mu) {
   const RowDir da = hs_affine(q, l, hdpa);
-  const double rhoA = l.DA * l.rpA - q.lA + (sigma_mu - da.dwA * da.dlA) / q.wA;
-  const double rhoB = l.DB * l.rpB - q.lB + (sigma_mu - da.dwB * da.dlB) / q.wB;
+  const double rhoA = l.DA * l.rpA - q.lA + (sigma_mu - da.dwA * da.dlA) * l.iwA;
+  const double rhoB = l.DB * l.rpB - q.lB + (sigma_mu - da.dwB * da.dlB) * l.iwB;
   return hs_dir(l, rhoA, rhoB, hdp);
 }
 
@@ -537,22 +640,46 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
   return t;
 }
 
-template <int NU>
+// Row sweep of one thread (lane = halfspace step, obstacles o = wave, wave + 4, ...): the rows
+// of kSweep obstacles are loaded together before any is processed, so kSweep x 8 independent
+// global loads are in flight instead of 8 (the passes are latency-bound at a few hundred rows per
+// thread).  Inside the body: q (the row), o, r (its workspace index).
+constexpr int kSweep = 2;
+#define ROW_SWEEP_BEGIN                                                              \
+  for (int o0_ = wave; o0_ < O; o0_ += kSweep * kWaves) {                            \
+    HsRow qs_[kSweep];                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < kSweep; ++i_) {                          \
+      const int o_ = o0_ + i_ * kWaves;                                              \
+      if (o_ < O) qs_[i_] = rows.load(static_cast<int64_t>(o_) * kRowStride + lane); \
+    }                                                                                \
+    _Pragma("unroll") for (int i_ = 0; i_ < kSweep; ++i_) {                          \
+      const int o = o0_ + i_ * kWaves;                                               \
+      if (o >= O) break;                                                             \
+      const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;                 \
+      (void)r;                                                                       \
+      const HsRow q = qs_[i_];
+#define ROW_SWEEP_END \
+  }                   \
+  }
+
+template <int NU, int NMAX>
 __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
   extern __shared__ double lds_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
-  const int n = a.n, H = a.H, K = a.K, O = a.O, ld = a.ld, nx = a.nx;
-  const Lds s = carve(lds_raw, n, H, ld);
+  const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
+  constexpr int ld = LdsPlan<NMAX>::ld;
+  const Lds s = carve<NMAX>(lds_raw);
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + b * a.ws_pp;
 #ifdef DRCVAR_MPC_STAMPS
   unsigned long long stamp_acc[kStampSlots] = {};
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
 #endif
+  // rows: [O][8 fields][64 steps] — one base, the field is an immediate offset
+  const RowArrays rows{ws, ws + kStepPad, ws + 2 * kStepPad, ws + 3 * kStepPad,
+                       ws + 4 * kStepPad, ws + 5 * kStepPad, ws + 6 * kStepPad, ws + 7 * kStepPad};
   const int64_t pitch = static_cast<int64_t>(O) * kStepPad;
-  const RowArrays rows{ws, ws + pitch, ws + 2 * pitch, ws + 3 * pitch,
-                       ws + 4 * pitch, ws + 5 * pitch, ws + 6 * pitch, ws + 7 * pitch};
   const double* x0 = a.x0 + b * a.x0_sp;
   const double* xr = a.xr + b * a.xr_sp;
 
@@ -584,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       const double* hp = a.hs_h + b * a.h_sp + o * a.h_so + lane * a.h_sk;
       const double g = a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk];
       const double h0 = hp[0], h1 = hp[1];
-      const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+      const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
       rows.h0[r] = h0;
       rows.h1[r] = h1;
       rows.g[r] = g;
@@ -644,12 +771,11 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       double gap = 0.0, rpm = 0.0, rdm = 0.0;
       if (lane < K) {
         const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-        for (int o = wave; o < O; o += kWaves) {
-          const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+        ROW_SWEEP_BEGIN
           const HsLin l = hs_lin(q, p0, p1);
-          const double om = l.DA * (kSlackHess + l.DB) / l.sig;
+          const double om = l.DA * (kSlackHess + l.DB) * l.isig;
           const double rhoA = l.DA * l.rpA - q.lA, rhoB = l.DB * l.rpB - q.lB;
-          const double coef = rhoA - l.DA * (-l.rds + rhoA + rhoB) / l.sig;
+          const double coef = rhoA - l.DA * (-l.rds + rhoA + rhoB) * l.isig;
           acc[0] += q.lA * q.h0;
           acc[1] += q.lA * q.h1;
           acc[2] += om * q.h0 * q.h0;
@@ -660,7 +786,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
           gap += q.wA * q.lA + q.wB * q.lB;
           rpm = fmax(rpm, fmax(fabs(l.rpA), fabs(l.rpB)));
           rdm = fmax(rdm, fabs(l.rds));
-        }
+        ROW_SWEEP_END
       }
 #pragma unroll
       for (int q = 0; q < kPerStepQ; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
@@ -743,7 +869,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - gp_transpose<NU>(s, s.za, j, H);
     __syncthreads();
     MPC_PHASE(2);
-    if (!cholesky(s, n, ld)) {
+    if (!cholesky<(NMAX + kTile - 1) / kTile>(s, n, ld)) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
@@ -759,11 +885,10 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     if (lane < K) {
       const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
       const double d0 = s.dpa[2 * lane], d1 = s.dpa[2 * lane + 1];
-      for (int o = wave; o < O; o += kWaves) {
-        const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+      ROW_SWEEP_BEGIN
         const HsLin l = hs_lin(q, p0, p1);
         amax = fmin(amax, hs_ratio(q, hs_affine(q, l, q.h0 * d0 + q.h1 * d1)));
-      }
+      ROW_SWEEP_END
     }
     if (a.has_u) {
       for (int j = tid; j < n; j += kBlock) {
@@ -790,21 +915,20 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       if (lane < K) {
         const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
         const double d0 = s.dpa[2 * lane], d1 = s.dpa[2 * lane + 1];
-        for (int o = wave; o < O; o += kWaves) {
-          const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+        ROW_SWEEP_BEGIN
           const HsLin l = hs_lin(q, p0, p1);
           const RowDir d = hs_affine(q, l, q.h0 * d0 + q.h1 * d1);
           gap_aff += (q.wA + a_aff * d.dwA) * (q.lA + a_aff * d.dlA) +
                      (q.wB + a_aff * d.dwB) * (q.lB + a_aff * d.dlB);
-          const double rhoA_b = l.DA * l.rpA - q.lA - d.dwA * d.dlA / q.wA;
-          const double rhoB_b = l.DB * l.rpB - q.lB - d.dwB * d.dlB / q.wB;
-          const double cb = rhoA_b - l.DA * (-l.rds + rhoA_b + rhoB_b) / l.sig;
-          const double cu = 1.0 / q.wA - l.DA * (1.0 / q.wA + 1.0 / q.wB) / l.sig;
+          const double rhoA_b = l.DA * l.rpA - q.lA - d.dwA * d.dlA * l.iwA;
+          const double rhoB_b = l.DB * l.rpB - q.lB - d.dwB * d.dlB * l.iwB;
+          const double cb = rhoA_b - l.DA * (-l.rds + rhoA_b + rhoB_b) * l.isig;
+          const double cu = l.iwA - l.DA * (l.iwA + l.iwB) * l.isig;
           acc[0] += cb * q.h0;
           acc[1] += cb * q.h1;
           acc[2] += cu * q.h0;
           acc[3] += cu * q.h1;
-        }
+        ROW_SWEEP_END
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
@@ -871,11 +995,10 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
       const double a0 = s.dpa[2 * lane], a1 = s.dpa[2 * lane + 1];
       const double d0 = s.dp[2 * lane], d1 = s.dp[2 * lane + 1];
-      for (int o = wave; o < O; o += kWaves) {
-        const HsRow q = rows.load(static_cast<int64_t>(o) * kStepPad + lane);
+      ROW_SWEEP_BEGIN
         const HsLin l = hs_lin(q, p0, p1);
         amax = fmin(amax, hs_ratio(q, hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu)));
-      }
+      ROW_SWEEP_END
     }
     if (a.has_u) {
       for (int j = tid; j < n; j += kBlock) {
@@ -900,9 +1023,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
       const double a0 = s.dpa[2 * lane], a1 = s.dpa[2 * lane + 1];
       const double d0 = s.dp[2 * lane], d1 = s.dp[2 * lane + 1];
-      for (int o = wave; o < O; o += kWaves) {
-        const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
-        const HsRow q = rows.load(r);
+      ROW_SWEEP_BEGIN
         const HsLin l = hs_lin(q, p0, p1);
         const RowDir d = hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu);
         rows.s[r] = q.sv + alpha * d.ds;
@@ -910,7 +1031,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
         rows.lA[r] = q.lA + alpha * d.dlA;
         rows.wB[r] = q.wB + alpha * d.dwB;
         rows.lB[r] = q.lB + alpha * d.dlB;
-      }
+      ROW_SWEEP_END
     }
     // box / position rows: every thread reads its own entries only, so no barrier is needed
     // between computing the direction and writing the update
@@ -966,7 +1087,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     // 2 = binding with s = 0 (equality, multiplier nu in [0, 50]); rows.s <- nu, rows.wA <- flag
     if (lane < K) {
       for (int o = wave; o < O; o += kWaves) {
-        const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+        const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
         const bool actA = rows.lA[r] > rows.wA[r], actB = rows.lB[r] > rows.wB[r];
         const double flag = actA ? (actB ? 2.0 : 1.0) : 0.0;
         rows.s[r] = flag == 2.0 ? rows.lA[r] : 0.0;
@@ -1003,7 +1124,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
         double acc[3] = {0, 0, 0};
         if (lane < K) {
           for (int o = wave; o < O; o += kWaves) {
-            const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+            const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             const double flag = rows.wA[r];
             const double wgt = flag == 1.0 ? kSlackHess : (flag == 2.0 ? kPolishRho : 0.0);
             const double h0 = rows.h0[r], h1 = rows.h1[r];
@@ -1034,7 +1155,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       assemble_hessian<NU>(s, H0, n, ld, H);
       __syncthreads();
       MPC_PHASE(10);
-      if (!cholesky(s, n, ld)) break;
+      if (!cholesky<(NMAX + kTile - 1) / kTile>(s, n, ld)) break;
       MPC_PHASE(11);
       for (int pass = 0; pass < kPolishIters; ++pass) {
         // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
@@ -1042,7 +1163,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
         if (lane < K) {
           const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
           for (int o = wave; o < O; o += kWaves) {
-            const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+            const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             const double flag = rows.wA[r];
             const double h0 = rows.h0[r], h1 = rows.h1[r];
             const double bb = h0 * c0 + h1 * c1 + rows.g[r];
@@ -1089,7 +1210,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
         if (lane < K) {
           const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
           for (int o = wave; o < O; o += kWaves) {
-            const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+            const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             if (rows.wA[r] == 2.0) rows.s[r] += kPolishRho * (rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r]);
           }
         }
@@ -1114,7 +1235,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       if (lane < K) {
         const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
         for (int o = wave; o < O; o += kWaves) {
-          const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+          const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
           const double flag = rows.wA[r];
           const double hp = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
           double nf = flag, nv = rows.s[r];
@@ -1216,7 +1337,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       // the optimal slack of a halfspace for the returned inputs is max(0, h.p + g)
       const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
       for (int o = wave; o < O; o += kWaves) {
-        const int64_t r = static_cast<int64_t>(o) * kStepPad + lane;
+        const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
         const double sv = fmax(0.0, rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r]);
         rows.s[r] = sv;
         obj += kSlackLin * sv + 0.5 * kSlackHess * sv * sv;
@@ -1260,18 +1381,26 @@ bool all_finite(const double* p, int64_t n) {
   return true;
 }
 
-template <int NU>
-int launch(const MpcArgs& args, int64_t n_problems, size_t lds_bytes, hipStream_t stream) {
+template <int NU, int NMAX>
+int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
+  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<NMAX>::total;
   static bool attr_set = false;  // idempotent; a racing second call sets the same value
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NMAX>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
     attr_set = true;
   }
-  hipLaunchKernelGGL(mpc_ipm_kernel<NU>, dim3(static_cast<unsigned>(n_problems)), dim3(kBlock),
-                     lds_bytes, stream, args);
+  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NMAX>), dim3(static_cast<unsigned>(n_problems)),
+                     dim3(kBlock), lds_bytes, stream, args);
   return DRCVAR_OK;
+}
+
+template <int NU>
+int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
+  return args.n <= 64 ? launch<NU, 64>(args, n_problems, stream)
+                      : launch<NU, 120>(args, n_problems, stream);
 }
 
 }  // namespace
@@ -1443,7 +1572,6 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
   args.n = nu * H;
   args.K = static_cast<int>(K);
   args.O = static_cast<int>(n_obstacles);
-  args.ld = args.n | 1;  // odd leading dimension: column walks hit distinct LDS banks
   args.has_u = model->has_input_bounds;
   args.has_p = model->has_position_bounds;
   for (int i = 0; i < DRCVAR_MPC_MAX_INPUTS; ++i) {
@@ -1478,17 +1606,15 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
   args.max_iter = max_iter;
   args.tol = tol;
   args.polish = polish;
-  const size_t lds_bytes = sizeof(double) * static_cast<size_t>(lds_doubles(args.n, H, args.ld));
-  if (lds_bytes > 160 * 1024) return DRCVAR_ERR_UNSUPPORTED;
 
   (void)hipGetLastError();
   auto st = static_cast<hipStream_t>(stream);
   int rc;
   switch (nu) {
-    case 1: rc = launch<1>(args, n_problems, lds_bytes, st); break;
-    case 2: rc = launch<2>(args, n_problems, lds_bytes, st); break;
-    case 3: rc = launch<3>(args, n_problems, lds_bytes, st); break;
-    default: rc = launch<4>(args, n_problems, lds_bytes, st); break;
+    case 1: rc = launch_nu<1>(args, n_problems, st); break;
+    case 2: rc = launch_nu<2>(args, n_problems, st); break;
+    case 3: rc = launch_nu<3>(args, n_problems, st); break;
+    default: rc = launch_nu<4>(args, n_problems, st); break;
   }
   if (rc != DRCVAR_OK) return rc;
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
