@@ -27,7 +27,8 @@ OFFLOAD_ARCH = os.environ.get("DRCVAR_OFFLOAD_ARCH", "gfx950")
 
 ABI_VERSION = 1
 OUT_WIDTH = 8
-MAX_SAMPLES = 16384
+MAX_SAMPLES = 16384               # largest unit held on chip (register plans)
+MAX_SAMPLES_STREAM = 2 ** 31 - 1  # larger units run the streaming kernel
 COL_MEAN_H0, COL_MEAN_H1, COL_G_MEAN, COL_H0, COL_H1, COL_G_CVAR, COL_G_DR_STAR, COL_G_DR_TILDE = range(8)
 
 # return codes (include/drcvar_halfspace.h)

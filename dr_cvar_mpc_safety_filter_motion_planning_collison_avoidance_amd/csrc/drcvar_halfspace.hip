@@ -495,6 +495,44 @@ __device__ __forceinline__ void select_from_memory(const double* base, int n, in
   *dsum_out = (s_below - n_below * (tau - mu_d)) + s_cand;
 }
 
+// compute_separating_vector(ego, mu) (core/geometry.py:35-53): (mu - ego) / |mu - ego|, [1, 0]
+// below 1e-10 (rsqrt + one Newton step; an infinite norm takes the IEEE path as diff / norm does)
+__device__ __forceinline__ void separating_direction(double mux, double muy, double e0, double e1,
+                                                     double deg_sq, double* h0, double* h1) {
+  const double dx = mux - e0, dy = muy - e1;
+  const double n2 = dx * dx + dy * dy;
+  const double inv = std::isfinite(n2) ? rsqrt_nr(n2) : 1.0 / sqrt(n2);
+  const bool degenerate = n2 < deg_sq;
+  *h0 = degenerate ? 1.0 : dx * inv;
+  *h1 = degenerate ? 0.0 : dy * inv;
+}
+
+// Offsets from the lower-tail statistics (wave 0, lane 0 writes).  L = tau + dsum / k.
+template <int NW>
+__device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, double h0, double h1,
+                                               double tau, double dsum, double mux, double muy,
+                                               int lane) {
+  const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);  // R_c |h| (risk_metrics.py:293, :234)
+  if (lane == 0) {
+    const double L = tau + dsum * prm.inv_k;  // lower-tail mean
+    const double g_cvar = r - prm.delta - L;
+    double g_star = kSentinel, g_tilde = kSentinel - r;
+    if (prm.epsilon >= 0.0) {  // else: DR LP unbounded (lambda -> inf), solver-failure sentinel
+      g_star = r - prm.delta + prm.eps_over_alpha - L;
+      g_tilde = g_star - r;
+    }
+    if constexpr (NW == 1) {
+      double m0, m1, g_mean;
+      mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
+      store_record(rec, m0, m1, g_mean, h0, h1, g_cvar, g_star, g_tilde);
+    } else {  // columns 0..2 are written by wave 1
+      reinterpret_cast<double*>(rec)[DRCVAR_COL_H0] = h0;
+      reinterpret_cast<double2*>(rec)[2] = make_double2(h1, g_cvar);
+      reinterpret_cast<double2*>(rec)[3] = make_double2(g_star, g_tilde);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
 //   BLOCK    threads per unit (one workgroup per unit)
@@ -595,13 +633,8 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   if constexpr (GIVEN_H) {
     h0 = e0;
     h1 = e1;
-  } else {  // compute_separating_vector(ego, mu), core/geometry.py:35-53
-    const double dx = mux - e0, dy = muy - e1;
-    const double n2 = dx * dx + dy * dy;
-    const double inv = std::isfinite(n2) ? rsqrt_nr(n2) : 1.0 / sqrt(n2);  // inf: as diff/norm
-    const bool degenerate = n2 < deg_sq;  // |mu - ego| < 1e-10 -> [1, 0]
-    h0 = degenerate ? 1.0 : dx * inv;
-    h1 = degenerate ? 0.0 : dy * inv;
+  } else {
+    separating_direction(mux, muy, e0, e1, deg_sq, &h0, &h1);
   }
   if (bad || prm.unbounded) {  // solver failure, risk_metrics.py:298-303,334-338
     if (tid == 0) {
@@ -715,26 +748,84 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   }
 
   // ---- 5. offsets (wave 0) -------------------------------------------------------------------
-  const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);  // R_c |h| (risk_metrics.py:293, :234)
-  if (lane == 0) {
-    const double L = tau + dsum * prm.inv_k;  // lower-tail mean
-    const double g_cvar = r - prm.delta - L;
-    double g_star = kSentinel, g_tilde = kSentinel - r;
-    if (prm.epsilon >= 0.0) {  // else: DR LP unbounded (lambda -> inf), solver-failure sentinel
-      g_star = r - prm.delta + prm.eps_over_alpha - L;
-      g_tilde = g_star - r;
-    }
-    if constexpr (NW == 1) {
-      double m0, m1, g_mean;
-      mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
-      store_record(rec, m0, m1, g_mean, h0, h1, g_cvar, g_star, g_tilde);
-    } else {  // columns 0..2 are written by wave 1 (below)
-      reinterpret_cast<double*>(rec)[DRCVAR_COL_H0] = h0;
-      reinterpret_cast<double2*>(rec)[2] = make_double2(h1, g_cvar);
-      reinterpret_cast<double2*>(rec)[3] = make_double2(g_star, g_tilde);
+  finish_offsets<NW>(rec, prm, h0, h1, tau, dsum, mux, muy, lane);
+  DRCVAR_STAMP(7);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// streaming variant for N > DRCVAR_MAX_SAMPLES: nothing is held in registers — the mean is a
+// strided pass over the unit's samples and the order statistic comes from select_from_memory's
+// exact histogram refinement over re-reads (min/max pass, ~1 histogram pass per factor 10^3 of
+// N, a candidate pass).  Any N up to 2^31 - 1; ~4 reads of the unit instead of 1.
+// ---------------------------------------------------------------------------------------------
+constexpr int kStreamBlock = 1024;
+constexpr int kStreamLogNB = 10;
+
+template <bool VEC, bool GIVEN_H>
+__global__ void __launch_bounds__(kStreamBlock)
+safe_halfspace_stream_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
+                             int64_t s_obs, int64_t s_step, int64_t s_samp,
+                             const double* __restrict__ dir, int64_t dir_s_obs,
+                             int64_t dir_s_step, Params prm, double* __restrict__ out) {
+  constexpr int BLOCK = kStreamBlock;
+  constexpr int NW = BLOCK / kWave;
+  constexpr int NB = 1 << kStreamLogNB;
+  __shared__ uint32_t hist[hist_words<NB>()];
+  __shared__ double cand[NW * kCap];
+  __shared__ uint32_t wcount[NW];
+  __shared__ double red_mom[2 * NW];
+  __shared__ double red_rng[2 * NW];
+  __shared__ double red_tail[NW];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = tid / kWave;
+  const int64_t u = blockIdx.x;
+  const int64_t o = u / n_steps;
+  const int64_t t = u - o * n_steps;
+  const double* base = samples + o * s_obs + t * s_step;
+  double* rec = out + u * DRCVAR_OUT_WIDTH;
+  double mom[2] = {0.0, 0.0};
+  for (int i = tid; i < n; i += BLOCK) {
+    const double* pt = base + static_cast<int64_t>(i) * s_samp;
+    if constexpr (VEC) {
+      const double2 v = *reinterpret_cast<const double2*>(pt);
+      mom[0] += v.x;
+      mom[1] += v.y;
+    } else {
+      mom[0] += pt[0];
+      mom[1] += pt[1];
     }
   }
-  DRCVAR_STAMP(7);
+  block_reduce<OpAdd, NW, 2>(mom, red_mom);
+  const double mux = mom[0] * prm.inv_n, muy = mom[1] * prm.inv_n;
+  const bool bad = !(std::isfinite(mom[0]) && std::isfinite(mom[1]));
+  const double* dp = dir + o * dir_s_obs + t * dir_s_step;
+  double h0, h1;
+  if constexpr (GIVEN_H) {
+    h0 = dp[0];
+    h1 = dp[1];
+  } else {
+    separating_direction(mux, muy, dp[0], dp[1], prm.degenerate_sq, &h0, &h1);
+  }
+  if (bad || prm.unbounded) {
+    if (tid == 0) {
+      const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);
+      double m0, m1, g_mean;
+      mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
+      store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
+    }
+    return;
+  }
+  const double mu_d = h0 * mux + h1 * muy;
+  double tau, dsum;
+  select_from_memory<BLOCK, kStreamLogNB, VEC>(base, n, s_samp, h0, h1, mu_d, prm.rank, hist,
+                                               cand, wcount, red_rng, red_tail, &tau, &dsum);
+  if (wave != 0) {
+    if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
+    return;
+  }
+  finish_offsets<NW>(rec, prm, h0, h1, tau, dsum, mux, muy, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -803,12 +894,33 @@ void launch_plan(Launch L, bool vec) {
 }
 
 template <bool GIVEN_H>
+void launch_stream(const Launch& L, bool vec) {
+  const dim3 grid(static_cast<unsigned>(L.units)), block(kStreamBlock);
+  if (vec) {
+    hipLaunchKernelGGL((safe_halfspace_stream_kernel<true, GIVEN_H>), grid, block, 0, L.stream,
+                       L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
+                       L.dir, L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+  } else {
+    hipLaunchKernelGGL((safe_halfspace_stream_kernel<false, GIVEN_H>), grid, block, 0, L.stream,
+                       L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
+                       L.dir, L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+  }
+}
+
+template <bool GIVEN_H>
 int dispatch(const Launch& L, int threads, int per) {
   if (L.units == 0) return DRCVAR_OK;
-  const int p = pick_plan(L.n, threads, per);
-  if (p < 0) return DRCVAR_ERR_UNSUPPORTED;
   const bool vec = (reinterpret_cast<uintptr_t>(L.samples) % 16 == 0) && (L.s_obs % 2 == 0) &&
                    (L.s_step % 2 == 0) && (L.s_samp % 2 == 0);
+  if (L.n > DRCVAR_MAX_SAMPLES) {  // beyond the register plans: the streaming kernel
+    if (threads != 0 || per != 0) return DRCVAR_ERR_UNSUPPORTED;
+    if (L.n > DRCVAR_MAX_SAMPLES_STREAM) return DRCVAR_ERR_UNSUPPORTED;
+    (void)hipGetLastError();
+    launch_stream<GIVEN_H>(L, vec);
+    return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
+  }
+  const int p = pick_plan(L.n, threads, per);
+  if (p < 0) return DRCVAR_ERR_UNSUPPORTED;
   (void)hipGetLastError();  // clear stale errors from unrelated work
   switch (p) {
     case 0: launch_plan<64, 2, 7, GIVEN_H>(L, vec); break;
@@ -922,7 +1034,7 @@ const char* drcvar_strerror(int code) {
   switch (code) {
     case DRCVAR_OK: return "ok";
     case DRCVAR_ERR_INVALID_ARGUMENT: return "invalid argument";
-    case DRCVAR_ERR_UNSUPPORTED: return "n_samples exceeds DRCVAR_MAX_SAMPLES or no such launch geometry";
+    case DRCVAR_ERR_UNSUPPORTED: return "n_samples beyond DRCVAR_MAX_SAMPLES_STREAM or no such launch geometry";
     case DRCVAR_ERR_LAUNCH: return "HIP kernel launch failed";
     default: return "unknown error";
   }
@@ -931,6 +1043,13 @@ const char* drcvar_strerror(int code) {
 int drcvar_launch_plan(int64_t n_samples, int32_t* threads_per_unit, int32_t* samples_per_thread,
                        int32_t* bins) {
   if (n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (n_samples > DRCVAR_MAX_SAMPLES) {  // streaming kernel: nothing per thread held on chip
+    if (n_samples > DRCVAR_MAX_SAMPLES_STREAM) return DRCVAR_ERR_UNSUPPORTED;
+    if (threads_per_unit) *threads_per_unit = kStreamBlock;
+    if (samples_per_thread) *samples_per_thread = 0;
+    if (bins) *bins = 1 << kStreamLogNB;
+    return DRCVAR_OK;
+  }
   const int p = pick_plan(n_samples, 0, 0);
   if (p < 0) return DRCVAR_ERR_UNSUPPORTED;
   if (threads_per_unit) *threads_per_unit = kPlans[p].block;

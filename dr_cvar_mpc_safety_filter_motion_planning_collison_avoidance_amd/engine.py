@@ -66,8 +66,8 @@ def _check_samples(samples: torch.Tensor, ndim: int) -> None:
     n = samples.shape[-2]
     if n < 1:
         raise ValueError("each unit needs at least one sample")
-    if n > _native.MAX_SAMPLES:
-        raise ValueError(f"n_samples={n} exceeds the engine limit {_native.MAX_SAMPLES}")
+    if n > _native.MAX_SAMPLES_STREAM:
+        raise ValueError(f"n_samples={n} exceeds the engine limit {_native.MAX_SAMPLES_STREAM}")
 
 
 def _check_pairs(t: torch.Tensor, name: str, rows: int, device: torch.device) -> None:

@@ -47,11 +47,15 @@ extern "C" {
 /* return codes */
 #define DRCVAR_OK 0
 #define DRCVAR_ERR_INVALID_ARGUMENT 1 /* null pointer, negative size, n_samples < 1, alpha <= 0, ... */
-#define DRCVAR_ERR_UNSUPPORTED 2      /* n_samples above DRCVAR_MAX_SAMPLES */
+#define DRCVAR_ERR_UNSUPPORTED 2      /* n_samples above DRCVAR_MAX_SAMPLES_STREAM, or an explicit
+                                         geometry that does not exist / cover n_samples */
 #define DRCVAR_ERR_LAUNCH 3           /* the HIP runtime refused the launch */
 
 /* largest n_samples a single unit may hold (samples are kept on chip, in registers) */
 #define DRCVAR_MAX_SAMPLES 16384
+/* larger units run a streaming kernel (samples re-read from memory instead of held on chip;
+   ~4 reads of the unit's samples instead of 1) up to this many samples */
+#define DRCVAR_MAX_SAMPLES_STREAM 2147483647
 
 /* output record columns */
 #define DRCVAR_COL_MEAN_H0 0    /* MeanSafeHalfspace.h[0]   (direction from the origin, halfspaces.py:88) */
@@ -112,7 +116,8 @@ int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n
 
 /*
  * Host-only query (no device access): the launch geometry chosen for n_samples — threads per
- * workgroup, samples held per thread and histogram bins.  Returns DRCVAR_OK or an error code.
+ * workgroup, samples held per thread (0 = the streaming kernel, n_samples > DRCVAR_MAX_SAMPLES)
+ * and histogram bins.  Returns DRCVAR_OK or an error code.
  */
 int drcvar_launch_plan(int64_t n_samples, int32_t* threads_per_unit, int32_t* samples_per_thread,
                        int32_t* bins);

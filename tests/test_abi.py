@@ -63,8 +63,13 @@ def test_launch_plan_rejects():
         _native.launch_plan(0)
     assert e.value.code == _native.ERR_INVALID_ARGUMENT
     with pytest.raises(_native.EngineError) as e:
-        _native.launch_plan(_native.MAX_SAMPLES + 1)
+        _native.launch_plan(_native.MAX_SAMPLES_STREAM + 1)
     assert e.value.code == _native.ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("n", [_native.MAX_SAMPLES + 1, 100_000, 10_000_000])
+def test_launch_plan_streaming_beyond_register_plans(n):
+    assert _native.launch_plan(n) == (1024, 0, 1024)
 
 
 def _call(lib, **kw):
@@ -86,7 +91,7 @@ def test_host_side_argument_validation():
     assert _call(lib, O=-1) == _native.ERR_INVALID_ARGUMENT
     assert _call(lib, samples=0) == _native.ERR_INVALID_ARGUMENT
     assert _call(lib, out=0) == _native.ERR_INVALID_ARGUMENT
-    assert _call(lib, N=_native.MAX_SAMPLES + 1) == _native.ERR_UNSUPPORTED
+    assert _call(lib, N=_native.MAX_SAMPLES_STREAM + 1) == _native.ERR_UNSUPPORTED
     # empty batches are a no-op (nothing is launched)
     assert _call(lib, O=0) == _native.OK
     assert _call(lib, T=0, samples=0, ego=0, out=0) == _native.OK

@@ -218,3 +218,45 @@ def test_every_geometry_agrees(n):
         launch, out = engine.prepare_safe_halfspaces(s, e, RiskParams(), geometry=g)
         launch()
         _assert_match(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("n", [16385, 20000, 65536, 250_000])
+def test_streaming_kernel_beyond_register_plans(n):
+    """N > DRCVAR_MAX_SAMPLES runs the streaming kernel (samples re-read, nothing on chip)."""
+    rng = np.random.default_rng(n)
+    O, T = 2, 2
+    samples = rng.normal(size=(O, T, n, 2)) * 0.1 + rng.uniform(-3, 3, size=(O, T, 1, 2))
+    ego = rng.uniform(-3, 3, size=(T, 2))
+    _assert_match(_run(samples, ego, RiskParams()),
+                  c_oracle.safe_halfspaces(samples, ego, 0.3, 0.3, 0.2, 0.1, 0.15))
+
+
+@pytest.mark.parametrize("alpha", [0.001, 0.2, 0.999, 1.5])
+def test_streaming_kernel_alpha_ties_and_sentinels(alpha):
+    rng = np.random.default_rng(7)
+    n = 40_000
+    samples = rng.normal(size=(3, 1, n, 2))
+    samples[1] = np.round(samples[1] * 2.0) / 2.0           # heavy ties
+    samples[2, 0, :, :] = 0.25                               # all equal
+    ego = np.array([[-2.0, 0.5]])
+    p = RiskParams(alpha=alpha)
+    _assert_match(_run(samples, ego, p),
+                  cf.safe_halfspaces(samples, ego, 0.3, 0.3, alpha, 0.1, 0.15))
+    bad = samples.copy()
+    bad[0, 0, 12345, 1] = np.nan
+    got = _run(bad, ego, p)
+    assert got[0, 0, 5] == 100.0
+
+
+def test_streaming_kernel_strided_layout():
+    rng = np.random.default_rng(3)
+    n, S = 17000, 4
+    traj = rng.normal(size=(2, n, S, 2)) * 0.2                # reference [O, N, S+1, 2] order
+    import torch
+    dev = torch.device("cuda", 0)
+    t = torch.as_tensor(traj).to(dev).permute(0, 2, 1, 3)    # [O, S, N, 2] view, strided
+    ego = rng.normal(size=(S, 2))
+    got = engine.safe_halfspaces(t, torch.as_tensor(ego).to(dev), RiskParams()).cpu().numpy()
+    want = c_oracle.safe_halfspaces(np.ascontiguousarray(np.transpose(traj, (0, 2, 1, 3))), ego,
+                                    0.3, 0.3, 0.2, 0.1, 0.15)
+    _assert_match(got, want)
