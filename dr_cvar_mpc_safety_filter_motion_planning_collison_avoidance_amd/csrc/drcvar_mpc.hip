@@ -364,7 +364,112 @@ __device__ inline void assemble_hessian(const Lds& s, const double* H0, int n, i
   }
 }
 
-// Right-looking LDL' factorisation of the lower triangle of K (n x n, leading dimension ld) with
+// Size class NMAX = 120.  Left-looking blocked LDL' of the lower triangle of K (n x n, leading dimension ld) with
+// UNSCALED columns: afterwards K[i][j] (i > j) = L_ij d_j and s.diag[j] = 1 / d_j.
+// Panels of 16 columns.  Per panel: (1) every thread quad updates a 4 x 4 block of the panel with
+// the previous panels, A[i][k] -= sum_{j<j0} C_ij C_kj / d_j (the j-sum split over the quad's four
+// threads, combined with xor shuffles); (2) wave 0 factors the panel with its rows in registers
+// (lane = row, two rows per lane), pivots and column entries travelling by readlane — no barrier
+// inside the panel.  Two barriers per panel instead of one per column, and no LDS
+// read-modify-write in the factorisation's inner loop.  Returns false on a non-positive or
+// non-finite pivot (uniform: the verdict goes through LDS).
+constexpr int kPanel = 16;
+constexpr int kTile = 16;  // triangular-solve block
+
+__device__ inline bool cholesky_blocked(const Lds& s, int n, int ld) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* K = s.K;
+  double* flag = s.sc + 62;
+  if (tid == 0) *flag = 0.0;
+  const int npanel = (n + kPanel - 1) / kPanel;
+  for (int J = 0; J < npanel; ++J) {
+    const int j0 = J * kPanel, j1 = min(j0 + kPanel, n), w = j1 - j0;
+    if (j0 > 0) {  // (1) update from the previous panels
+      const int nitems = ((n - j0 + 3) >> 2) * (kPanel / 4);
+      const int q = tid & 3;
+      for (int item = tid >> 2; item < nitems; item += kBlock >> 2) {
+        const int rb = item >> 2, cb = item & 3;
+        if (cb > rb) continue;  // strictly above the diagonal block (uniform within the quad)
+        const int i0 = j0 + 4 * rb, k0 = j0 + 4 * cb;
+        double acc[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+        for (int j = q; j < j0; j += 4) {
+          const double dj = s.diag[j];
+          double ci[4], ck[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ci[r] = i0 + r < n ? K[(i0 + r) * ld + j] : 0.0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ck[c] = k0 + c < j1 ? K[(k0 + c) * ld + j] * dj : 0.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] += ci[r] * ck[c];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            acc[r][c] += __shfl_xor(acc[r][c], 1);
+            acc[r][c] += __shfl_xor(acc[r][c], 2);
+          }
+        if (q == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const int i = i0 + r, k = k0 + c;
+              if (i < n && k < j1 && k <= i) K[i * ld + k] -= acc[r][c];
+            }
+        }
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // (2) factor the panel, rows j0 + lane and j0 + 64 + lane
+      const int r0 = j0 + lane, r1 = j0 + 64 + lane;
+      double a0[kPanel], a1[kPanel];
+#pragma unroll
+      for (int c = 0; c < kPanel; ++c) {
+        a0[c] = (c < w && r0 < n && j0 + c <= r0) ? K[r0 * ld + j0 + c] : 0.0;
+        a1[c] = (c < w && r1 < n) ? K[r1 * ld + j0 + c] : 0.0;
+      }
+      bool ok = true;
+#pragma unroll
+      for (int c = 0; c < kPanel; ++c) {
+        if (c < w && ok) {
+          const double d = readlane_f64(a0[c], c);
+          if (!(d > 0.0) || !isfinite(d)) {
+            ok = false;
+          } else {
+            const double invd = 1.0 / d;
+            if (lane == 0) s.diag[j0 + c] = invd;
+#pragma unroll
+            for (int k = c + 1; k < kPanel; ++k) {
+              if (k < w) {
+                const double akc = readlane_f64(a0[c], k) * invd;
+                if (r0 >= j0 + k) a0[k] -= a0[c] * akc;
+                a1[k] -= a1[c] * akc;
+              }
+            }
+          }
+        }
+      }
+      if (!ok && lane == 0) *flag = 1.0;
+#pragma unroll
+      for (int c = 0; c < kPanel; ++c) {
+        if (c < w && r0 < n && j0 + c <= r0) K[r0 * ld + j0 + c] = a0[c];
+        if (c < w && r1 < n) K[r1 * ld + j0 + c] = a1[c];
+      }
+    }
+    __syncthreads();
+    if (*flag != 0.0) return false;  // uniform
+  }
+  return true;
+}
+
+// Size class NMAX <= 64.  Right-looking LDL' factorisation of the lower triangle of K (n x n, leading dimension ld) with
 // UNSCALED columns: afterwards K[i][j] (i > j) = L_ij d_j and s.diag[j] = 1 / d_j.
 // The matrix lives in REGISTERS during the factorisation: thread (tr, tc) of a 16 x 16 grid owns
 // the elements K[tr + 16a][tc + 16b] (a, b < 8, so n <= 128), 64 doubles, statically indexed.
@@ -375,10 +480,9 @@ __device__ inline void assemble_hessian(const Lds& s, const double* H0, int n, i
 // per column.  Row groups a whose rows are all above the trailing part are skipped (the test is
 // uniform across a wave except within one 4-row window).  The factor is written back to LDS for
 // the solves.  Returns false on a non-positive or non-finite pivot (uniform).
-constexpr int kTile = 16;
 
 template <int kOwn>
-__device__ inline bool cholesky(const Lds& s, int n, int ld) {
+__device__ inline bool cholesky_tiled(const Lds& s, int n, int ld) {
   static_assert(kBlock == kTile * kTile && kOwn <= 8, "tile grid");
   const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
   double* K = s.K;
@@ -448,6 +552,19 @@ __device__ inline bool cholesky(const Lds& s, int n, int ld) {
     }
   __syncthreads();
   return true;
+}
+
+
+// Measured per factorisation (shader cycles): the register-tiled form wins for n <= 64 (one
+// barrier per column is cheap there), the blocked form for n ~ 100 (fewer barriers, panel work
+// off the critical path of three waves).
+template <int NMAX>
+__device__ inline bool cholesky(const Lds& s, int n, int ld) {
+  if constexpr (NMAX <= 64) {
+    return cholesky_tiled<(NMAX + kTile - 1) / kTile>(s, n, ld);
+  } else {
+    return cholesky_blocked(s, n, ld);
+  }
 }
 
 // Solve K x = b with the factor above, b in x[0..n) (LDS).  Blocked by 16: the diagonal block is
@@ -869,7 +986,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
     for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - gp_transpose<NU>(s, s.za, j, H);
     __syncthreads();
     MPC_PHASE(2);
-    if (!cholesky<(NMAX + kTile - 1) / kTile>(s, n, ld)) {
+    if (!cholesky<NMAX>(s, n, ld)) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
@@ -1155,7 +1272,7 @@ __global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
       assemble_hessian<NU>(s, H0, n, ld, H);
       __syncthreads();
       MPC_PHASE(10);
-      if (!cholesky<(NMAX + kTile - 1) / kTile>(s, n, ld)) break;
+      if (!cholesky<NMAX>(s, n, ld)) break;
       MPC_PHASE(11);
       for (int pass = 0; pass < kPolishIters; ++pass) {
         // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
