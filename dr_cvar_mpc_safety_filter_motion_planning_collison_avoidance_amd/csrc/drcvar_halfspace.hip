@@ -113,15 +113,73 @@ struct OpMax {
   __device__ static double f(double a, double b) { return fmax(a, b); }
 };
 
-// Result is uniform across the wave.  Requires all 64 lanes active.
+// gfx950 lane swaps: permlane16_swap exchanges odd rows of its first operand with even rows of
+// its second, permlane32_swap the upper half of the first with the lower half of the second.
+// With both operands = v, element [0] holds rows (0,0,2,2) / halves (lo,lo) and element [1] rows
+// (1,1,3,3) / halves (hi,hi), so Op([0], [1]) combines row pairs / halves in every lane at once.
+// a wave-uniform value moved to SGPRs (keeps uniform scalars out of the VGPR budget)
+__device__ __forceinline__ double uniform_f64(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float uniform_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+template <class Op>
+__device__ __forceinline__ double swap_combine16(double v) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return Op::f(__hiloint2double(hi[0], lo[0]), __hiloint2double(hi[1], lo[1]));
+}
+template <class Op>
+__device__ __forceinline__ double swap_combine32(double v) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return Op::f(__hiloint2double(hi[0], lo[0]), __hiloint2double(hi[1], lo[1]));
+}
+
+// Result is uniform across the wave (bitwise: every lane evaluates the same tree,
+// ((r0 + r1) + (r2 + r3)) over the row results).  Requires all 64 lanes active.
+// Measured (scripts/micro/reduce.hip): ~190 cycles latency, ~150 cycles per extra independent value.
 template <class Op>
 __device__ __forceinline__ double wave_reduce(double v) {
   v = Op::f(v, dpp_f64<kDppQuadXor1>(v));
   v = Op::f(v, dpp_f64<kDppQuadXor2>(v));
   v = Op::f(v, dpp_f64<kDppHalfMirror>(v));
   v = Op::f(v, dpp_f64<kDppMirror>(v));
-  return Op::f(Op::f(readlane_f64(v, 0), readlane_f64(v, 16)),
-               Op::f(readlane_f64(v, 32), readlane_f64(v, 48)));
+  return uniform_f64(swap_combine32<Op>(swap_combine16<Op>(v)));
+}
+
+// fp32 sum over the wave, same tree (the DPP moves fold into v_add_f32_dpp): ~60 cycles per value.
+__device__ __forceinline__ float wave_sum_f32(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kDppQuadXor1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kDppQuadXor2, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kDppHalfMirror, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kDppMirror, 0xF, 0xF, false));
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = __int_as_float(a[0]) + __int_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return uniform_f32(__int_as_float(b[0]) + __int_as_float(b[1]));
+}
+
+// Sum of NW per-wave partials p[0..NW) read by every thread (broadcast LDS reads), fixed
+// pairwise tree — cheaper than a second wave reduction for the small NW of the launch plans.
+template <int NW, class T>
+__device__ __forceinline__ T sum_partials(const T* p) {
+  T v[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) v[w] = p[w];
+#pragma unroll
+  for (int stride = 1; stride < NW; stride *= 2)
+#pragma unroll
+    for (int w = 0; w + stride < NW; w += 2 * stride) v[w] = v[w] + v[w + stride];
+  if constexpr (sizeof(T) == 8) {
+    return uniform_f64(v[0]);
+  } else {
+    return uniform_f32(v[0]);
+  }
 }
 
 template <class Op>
@@ -153,6 +211,32 @@ __device__ __forceinline__ void block_reduce(double (&v)[K], double* slot) {
       const double part = lane < NW ? slot[q * NW + lane] : identity_of<Op>();
       v[q] = wave_reduce<Op>(part);
     }
+  }
+}
+
+// Workgroup sums of the load phase: KD fp64 values (the mean sums) and KF fp32 values (the
+// pivot-shifted second moments, which only position the histogram window).  One barrier.
+template <int NW, int KD, int KF>
+__device__ __forceinline__ void block_sum_moments(double (&v)[KD], float (&f)[KF], double* slot_d,
+                                                  float* slot_f) {
+#pragma unroll
+  for (int q = 0; q < KD; ++q) v[q] = wave_reduce<OpAdd>(v[q]);
+#pragma unroll
+  for (int q = 0; q < KF; ++q) f[q] = wave_sum_f32(f[q]);
+  if constexpr (NW > 1) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < KD; ++q) slot_d[q * NW + w] = v[q];
+#pragma unroll
+      for (int q = 0; q < KF; ++q) slot_f[q * NW + w] = f[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KD; ++q) v[q] = sum_partials<NW>(slot_d + q * NW);
+#pragma unroll
+    for (int q = 0; q < KF; ++q) f[q] = sum_partials<NW>(slot_f + q * NW);
   }
 }
 
@@ -341,7 +425,7 @@ __device__ __forceinline__ void append_candidate(double* region, uint32_t& wbase
 // per-wave regions cand[w * kCap + i], i < wcount[w] (global order: wave, then position — fixed).
 // Candidates are pulled into registers (g = lane, lane + 64) and compared through readlane, so
 // the O(c^2) ranking never waits on LDS.  Also returns s_cand = sum over candidates below tau of
-// (cand - tau), reduced in fixed order.
+// (cand - tau), accumulated in candidate order.
 template <int NW>
 __device__ __forceinline__ double rank_candidates(const double* cand, const uint32_t* wcount,
                                                   uint32_t c, uint32_t rr, int lane,
@@ -363,41 +447,45 @@ __device__ __forceinline__ double rank_candidates(const double* cand, const uint
 #pragma unroll
   for (int q = 0; q < 2; ++q)
     if (slot[q] >= 0) mine[q] = cand[slot[q]];
+  // per candidate v (lane-parallel): #{z < v}, #{z == v} and sum_{z < v} (z - v); the lane of
+  // tau then holds s_cand itself, so no reduction follows the ranking
   uint32_t less[2] = {0u, 0u}, eq[2] = {0u, 0u};
+  double sl[2] = {0.0, 0.0};
   const uint32_t c0 = c < kWave ? c : kWave;
   for (uint32_t i = 0; i < c0; ++i) {  // uniform trip count
     const double z = readlane_f64(mine[0], static_cast<int>(i));
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      less[q] += (z < mine[q]) ? 1u : 0u;
+      const bool lt = z < mine[q];
+      less[q] += lt ? 1u : 0u;
       eq[q] += (z == mine[q]) ? 1u : 0u;
+      sl[q] += lt ? z - mine[q] : 0.0;
     }
   }
   for (uint32_t i = kWave; i < c; ++i) {
     const double z = readlane_f64(mine[1], static_cast<int>(i - kWave));
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      less[q] += (z < mine[q]) ? 1u : 0u;
+      const bool lt = z < mine[q];
+      less[q] += lt ? 1u : 0u;
       eq[q] += (z == mine[q]) ? 1u : 0u;
+      sl[q] += lt ? z - mine[q] : 0.0;
     }
   }
   bool found = false;
-  double found_v = 0.0;
+  double found_v = 0.0, found_s = 0.0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     if (lane + q * kWave < c && less[q] <= rr && rr < less[q] + eq[q]) {
       found = true;
       found_v = mine[q];
+      found_s = sl[q];
     }
   }
   const unsigned long long fb = __ballot(found);
-  const double tau = readlane_f64(found_v, __ffsll(static_cast<long long>(fb)) - 1);
-  double part = 0.0;
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-    if (mine[q] < tau) part += mine[q] - tau;
-  *s_cand = wave_reduce<OpAdd>(part);
-  return tau;
+  const int src = __ffsll(static_cast<long long>(fb)) - 1;
+  *s_cand = readlane_f64(found_s, src);
+  return readlane_f64(found_v, src);
 }
 
 // Exact selection for the units the register fast path does not finish (degenerate moments, or a
@@ -487,7 +575,7 @@ __device__ __forceinline__ void select_from_memory(const double* base, int n, in
   }
   __syncthreads();
   if (wave != 0) return;
-  const double s_below = wave_reduce<OpAdd>(lane < NW ? red_tail[lane] : 0.0);
+  const double s_below = sum_partials<NW>(red_tail);
   double s_cand = 0.0;
   if (!tau_known) tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
   const double n_below = static_cast<double>(rank - rr);
@@ -507,12 +595,23 @@ __device__ __forceinline__ void separating_direction(double mux, double muy, dou
   *h1 = degenerate ? 0.0 : dy * inv;
 }
 
+// |h| for R_c |h| (risk_metrics.py:293, :234).  h is a unit vector up to rounding on the
+// separating-direction path, where sqrt(1 + e) = 1 + e/2 - e^2/8 (+ O(e^3)) replaces the long
+// fp64 sqrt sequence (e = |h|^2 - 1 is exact there; the result is within 1 ulp of the correctly
+// rounded sqrt — it can differ only where 1 + e/2 is a rounding tie); any other h takes sqrt.
+__device__ __forceinline__ double norm_h(double h0, double h1) {
+  const double n2 = h0 * h0 + h1 * h1;
+  const double e = n2 - 1.0;
+  if (fabs(e) < 0x1p-40) return 1.0 + fma(-0.125 * e, e, 0.5 * e);  // uniform branch
+  return sqrt(n2);
+}
+
 // Offsets from the lower-tail statistics (wave 0, lane 0 writes).  L = tau + dsum / k.
+// r = R_c |h| (risk_metrics.py:293, :234), computed by the caller as soon as h is known.
 template <int NW>
-__device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, double h0, double h1,
-                                               double tau, double dsum, double mux, double muy,
-                                               int lane) {
-  const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);  // R_c |h| (risk_metrics.py:293, :234)
+__device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, double r, double h0,
+                                               double h1, double tau, double dsum, double mux,
+                                               double muy, int lane) {
   if (lane == 0) {
     const double L = tau + dsum * prm.inv_k;  // lower-tail mean
     const double g_cvar = r - prm.delta - L;
@@ -553,7 +652,8 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   __shared__ double cand[NW * kCap];
   __shared__ uint32_t wcount[NW];
   __shared__ uint32_t wbelow_sh[NW];
-  __shared__ double red_mom[7 * NW];
+  __shared__ double red_mom[2 * NW];
+  __shared__ float red_mom0[5 * NW];
   __shared__ double red_rng[2 * NW];
   __shared__ double red_tail[NW];
 
@@ -599,10 +699,13 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double z_alpha = prm.z_alpha, window_sd = prm.window_sd, hist_scale = prm.hist_scale;
   asm volatile("" ::"s"(e0), "s"(e1), "s"(inv_n), "s"(inv_n0), "s"(deg_sq), "s"(z_alpha),
                "s"(window_sd), "s"(hist_scale));
-  // Sums for the mean over every sample (plain sums, as np.mean); second moments over row 0 only
-  // (the first BLOCK samples) — they merely position the fast-path window, so a subsample is
-  // enough and cancellation in them can only cost speed, never exactness.
-  double mom[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // Sx Sy | Sx0 Sy0 Sxx0 Syy0 Sxy0
+  // Sums for the mean over every sample (plain sums, as np.mean, in fp64); second moments over
+  // row 0 only (the first BLOCK samples), shifted by the unit's first sample and summed in fp32 —
+  // they merely position the fast-path window, so a subsample at low precision is enough: an
+  // inaccurate window can only cost speed (the exact fallback), never exactness.
+  const double px = base[0], py = base[1];  // pivot (uniform scalar load)
+  double mom[2] = {0.0, 0.0};               // Sx Sy
+  float mom0[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // row 0, pivot-shifted: Sa Sb Saa Sbb Sab
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const bool valid = tid + j * BLOCK < n;
@@ -610,21 +713,23 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     mom[0] += a;
     mom[1] += b;
     if (j == 0) {
-      mom[2] = a;
-      mom[3] = b;
-      mom[4] = a * a;
-      mom[5] = b * b;
-      mom[6] = a * b;
+      const float fa = valid ? static_cast<float>(x[0] - px) : 0.f;
+      const float fb = valid ? static_cast<float>(y[0] - py) : 0.f;
+      mom0[0] = fa;
+      mom0[1] = fb;
+      mom0[2] = fa * fa;
+      mom0[3] = fb * fb;
+      mom0[4] = fa * fb;
     }
   }
   DRCVAR_STAMP(1);
-  block_reduce<OpAdd, NW, 7>(mom, red_mom);                              // [barrier 1]
+  block_sum_moments<NW>(mom, mom0, red_mom, red_mom0);                   // [barrier 1]
   DRCVAR_STAMP(2);
   const double mux = mom[0] * inv_n, muy = mom[1] * inv_n;
   // any non-finite sample makes a sum non-finite (so do sums that overflow): solver failure
   const bool bad = !(std::isfinite(mom[0]) && std::isfinite(mom[1]));
 #if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 1
-  if (tid == 0) rec[0] = mux + muy + mom[2] + mom[3] + mom[4] + mom[5];  // diagnostic: load+moments
+  if (tid == 0) rec[0] = mux + muy + mom0[0] + mom0[1] + mom0[2] + mom0[3];  // diagnostic
   return;
 #endif
 
@@ -636,9 +741,10 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   } else {
     separating_direction(mux, muy, e0, e1, deg_sq, &h0, &h1);
   }
+  const double rch = prm.rc * norm_h(h0, h1);  // R_c |h|
   if (bad || prm.unbounded) {  // solver failure, risk_metrics.py:298-303,334-338
     if (tid == 0) {
-      const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);
+      const double r = rch;
       double m0, m1, g_mean;
       mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
       store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
@@ -652,9 +758,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   for (int j = 0; j < P; ++j)  // +inf padding: never below, inside or a candidate
     d[j] = (tid + j * BLOCK < n) ? project(h0, h1, x[j], y[j]) : INFINITY;
   const double mu_d = h0 * mux + h1 * muy;
-  const double ma0 = mom[2] * inv_n0, mb0 = mom[3] * inv_n0;  // row-0 covariance
-  const double cxx = mom[4] * inv_n0 - ma0 * ma0, cyy = mom[5] * inv_n0 - mb0 * mb0;
-  const double cxy = mom[6] * inv_n0 - ma0 * mb0;
+  const double ma0 = mom0[0] * inv_n0, mb0 = mom0[1] * inv_n0;  // row-0 covariance
+  const double cxx = mom0[2] * inv_n0 - ma0 * ma0, cyy = mom0[3] * inv_n0 - mb0 * mb0;
+  const double cxy = mom0[4] * inv_n0 - ma0 * mb0;
   const double var_d = h0 * h0 * cxx + 2.0 * h0 * h1 * cxy + h1 * h1 * cyy;
   // window [wlo, whi] = mean_d + (z_alpha -+ window_sd) sd_d; only samples inside it are
   // histogrammed (LDS atomics), samples below it are counted with ballots.  Any positive scale
@@ -734,7 +840,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
     }
-    const double s_below = wave_reduce<OpAdd>(lane < NW ? red_tail[lane] : 0.0);
+    const double s_below = sum_partials<NW>(red_tail);
     double s_cand;
     tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
     dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
@@ -748,7 +854,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   }
 
   // ---- 5. offsets (wave 0) -------------------------------------------------------------------
-  finish_offsets<NW>(rec, prm, h0, h1, tau, dsum, mux, muy, lane);
+  finish_offsets<NW>(rec, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
   DRCVAR_STAMP(7);
 }
 
@@ -808,9 +914,10 @@ safe_halfspace_stream_kernel(const double* __restrict__ samples, int64_t n_steps
   } else {
     separating_direction(mux, muy, dp[0], dp[1], prm.degenerate_sq, &h0, &h1);
   }
+  const double rch = prm.rc * norm_h(h0, h1);  // R_c |h|
   if (bad || prm.unbounded) {
     if (tid == 0) {
-      const double r = prm.rc * sqrt(h0 * h0 + h1 * h1);
+      const double r = rch;
       double m0, m1, g_mean;
       mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
       store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
@@ -825,7 +932,7 @@ safe_halfspace_stream_kernel(const double* __restrict__ samples, int64_t n_steps
     if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
     return;
   }
-  finish_offsets<NW>(rec, prm, h0, h1, tau, dsum, mux, muy, lane);
+  finish_offsets<NW>(rec, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
