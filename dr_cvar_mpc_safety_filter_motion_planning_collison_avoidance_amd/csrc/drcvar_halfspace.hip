@@ -401,16 +401,12 @@ __device__ __forceinline__ double project_at(const double* base, int i, int64_t 
   }
 }
 
-// Value-linear bucket map of the fast-path window [lo, lo + NB/scale]: monotone for any
-// scale > 0.  Values below the window map to bins <= 0, values above (and the +inf padding) to
-// NB - 1; callers test window membership separately where it matters.
-template <int NB>
+// Value-linear position in the fast-path window: t(d) = d * scale + off (one fma, rounded once,
+// so monotone non-decreasing in d for any scale > 0).  Below the window: t < 0; inside: 0 <= t <
+// NB (bin = trunc(t) <= NB - 1); above it (and the +inf padding): t >= NB.
 struct LinearMap {
-  double lo, scale;
-  __device__ __forceinline__ int operator()(double d) const {
-    const int b = static_cast<int>(fmin((d - lo) * scale, static_cast<double>(NB - 1)));
-    return b;
-  }
+  double scale, off;
+  __device__ __forceinline__ double operator()(double d) const { return fma(d, scale, off); }
 };
 
 // Per-wave ordered compaction step: append the candidates of one row to this wave's LDS region.
@@ -762,16 +758,17 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double cxx = mom0[2] * inv_n0 - ma0 * ma0, cyy = mom0[3] * inv_n0 - mb0 * mb0;
   const double cxy = mom0[4] * inv_n0 - ma0 * mb0;
   const double var_d = h0 * h0 * cxx + 2.0 * h0 * h1 * cxy + h1 * h1 * cyy;
-  // window [wlo, whi] = mean_d + (z_alpha -+ window_sd) sd_d; only samples inside it are
-  // histogrammed (LDS atomics), samples below it are counted with ballots.  Any positive scale
-  // keeps the map monotone, so the approximate reciprocal square root is exact enough.
+  // window [wlo, wlo + 2 window_sd sd_d), wlo = mean_d + (z_alpha - window_sd) sd_d; only
+  // samples inside it are histogrammed (LDS atomics), samples below it are counted with ballots.
+  // Any positive scale keeps the map monotone, so the approximate reciprocal sqrt is exact enough.
   const double inv_sd = rsqrt_nr(var_d);
   const double sd_d = var_d * inv_sd;
   const double wlo = mu_d + (z_alpha - window_sd) * sd_d;
-  const double whi = mu_d + (z_alpha + window_sd) * sd_d;
-  const LinearMap<NB> map{wlo, prm.hist_scale * inv_sd};
+  const double scale = prm.hist_scale * inv_sd;
+  const LinearMap map{scale, -wlo * scale};
   const uint32_t rank = prm.rank;
-  bool fast = var_d > 0.0 && std::isfinite(map.scale) && std::isfinite(wlo) && map.scale > 0.0;
+  bool fast = var_d > 0.0 && std::isfinite(map.scale) && std::isfinite(map.off) && map.scale > 0.0;
+  constexpr double kNB = static_cast<double>(NB);
   uint32_t rr = rank, c = 0;
   int bin = 0;
   // per-sample bucket codes, two 16-bit codes per register: the bin inside the window, 0xFFFF
@@ -784,11 +781,12 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const double v = d[j];
-      const bool low = v < wlo;
+      const double tv = map(v);
+      const bool low = tv < 0.0;
       wbelow += static_cast<uint32_t>(__popcll(__ballot(low)));
       sq += low ? v - mu_d : 0.0;
-      const bool inw = !low && v <= whi;
-      const int b = map(v);
+      const bool inw = !low && tv < kNB;
+      const int b = inw ? static_cast<int>(tv) : 0;  // 0 <= b <= NB - 1 inside the window
       if (inw) atomicAdd(&hist[hist_slot<NB>(b)], 1u);
       const uint32_t cj = inw ? static_cast<uint32_t>(b) : 0xFFFFu;
       if (j % 2 == 0) code[j / 2] = cj;
