@@ -88,11 +88,26 @@ _lib = None
 def build(verbose: bool = False, extra_flags=()) -> str:
     """Compile the engine for gfx950 with hipcc into ``_lib/`` (works without a GPU)."""
     os.makedirs(LIB_DIR, exist_ok=True)
-    cmd = ["hipcc", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-I", INCLUDE_DIR, *extra_flags, *SOURCES, "-o", LIB_PATH + ".tmp"]
+    # one hipcc per source, concurrently (the halfspace kernel's template plans dominate), then
+    # one link: the library is the same as a single-command build
+    objs = [os.path.join(LIB_DIR, os.path.basename(src) + ".o") for src in SOURCES]
+    procs = []
+    for src, obj in zip(SOURCES, objs):
+        cmd = ["hipcc", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
+               "-I", INCLUDE_DIR, *extra_flags, src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd)))
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    link = ["hipcc", f"--offload-arch={OFFLOAD_ARCH}", "-shared", "-fPIC", *objs,
+            "-o", LIB_PATH + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        print(" ".join(link))
+    subprocess.run(link, check=True)
+    for obj in objs:
+        os.remove(obj)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 

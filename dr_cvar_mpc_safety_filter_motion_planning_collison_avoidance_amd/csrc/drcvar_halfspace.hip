@@ -40,6 +40,9 @@ constexpr int kWave = 64;
 constexpr int kCap = 128;          // candidates ranked directly (per-wave region size in LDS)
 constexpr int kMaxValueIters = 3;  // value-linear refinements before switching to integer keys
 constexpr double kSentinel = 100.0;
+constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2;  // sample load forms (kernel template)
+constexpr int64_t kNtBytes = 256ll << 20;  // launches reading more than the MALL use kLoadNt
+typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 #ifdef DRCVAR_STAMPS
 // diagnostic build only: per-unit shader-clock stamps at phase boundaries (wave 0)
@@ -633,10 +636,12 @@ __device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, d
 //   BLOCK    threads per unit (one workgroup per unit)
 //   P        samples held per thread (N <= BLOCK * P)
 //   LOG_NB   log2 of histogram bins
-//   VEC      every (x, y) pair is 16-B aligned -> one 16-B load per sample
+//   LOAD     kLoadPair: two 8-B loads per sample; kLoadVec: every (x, y) pair is 16-B aligned ->
+//            one 16-B load per sample; kLoadNt: the same, nontemporal (launches larger than the
+//            256 MB Infinity Cache, whose samples are streamed exactly once)
 //   GIVEN_H  `dir` holds h per unit (cvar_halfspace / dr_cvar_halfspace) instead of ego per step
 // ---------------------------------------------------------------------------------------------
-template <int BLOCK, int P, int LOG_NB, bool VEC, bool GIVEN_H>
+template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
 __global__ void __launch_bounds__(BLOCK)
 safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
                       int64_t s_obs, int64_t s_step, int64_t s_samp,
@@ -677,7 +682,11 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   for (int j = 0; j < P; ++j) {
     const int i = tid + j * BLOCK;
     const int64_t off = static_cast<int64_t>(i < n ? i : n - 1) * s_samp;
-    if constexpr (VEC) {
+    if constexpr (LOAD == kLoadNt) {  // streamed once: keep it out of L2 / MALL
+      const dbl2 v = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(base + off));
+      x[j] = v.x;
+      y[j] = v.y;
+    } else if constexpr (LOAD == kLoadVec) {
       const double2 v = *reinterpret_cast<const double2*>(base + off);
       x[j] = v.x;
       y[j] = v.y;
@@ -843,8 +852,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
     dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
   } else [[unlikely]] {
-    select_from_memory<BLOCK, LOG_NB, VEC>(base, n, s_samp, h0, h1, mu_d, rank, hist, cand,
-                                           wcount, red_rng, red_tail, &tau, &dsum);
+    select_from_memory<BLOCK, LOG_NB, LOAD != kLoadPair>(base, n, s_samp, h0, h1, mu_d, rank,
+                                                         hist, cand, wcount, red_rng, red_tail,
+                                                         &tau, &dsum);
     if (wave != 0) {
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
@@ -982,19 +992,27 @@ struct Launch {
   hipStream_t stream;
 };
 
+template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
+void launch_form(const Launch& L) {
+  hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
+                     dim3(static_cast<unsigned>(L.units)), dim3(BLOCK), 0, L.stream, L.samples,
+                     L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
+                     L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+}
+
 template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
 void launch_plan(Launch L, bool vec) {
-  const dim3 grid(static_cast<unsigned>(L.units)), block(BLOCK);
   L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < BLOCK ? L.n : BLOCK);
   L.prm.hist_scale = static_cast<double>(1 << LOG_NB) / (2.0 * L.prm.window_sd);
-  if (vec) {
-    hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, true, GIVEN_H>), grid, block, 0,
-                       L.stream, L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
-                       L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+  // measured on C5 (2.05 GB): nontemporal 16-B loads 0.746 of HBM peak vs 0.715; on C3 (3.2 MB,
+  // cache-resident across steps) they cost 3 %, so only launches larger than the MALL use them
+  const bool nt = vec && L.units * L.n * 16 > kNtBytes;
+  if (nt) {
+    launch_form<BLOCK, P, LOG_NB, kLoadNt, GIVEN_H>(L);
+  } else if (vec) {
+    launch_form<BLOCK, P, LOG_NB, kLoadVec, GIVEN_H>(L);
   } else {
-    hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, false, GIVEN_H>), grid, block, 0,
-                       L.stream, L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
-                       L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+    launch_form<BLOCK, P, LOG_NB, kLoadPair, GIVEN_H>(L);
   }
 }
 

@@ -19,7 +19,8 @@
  *   s.t. x_0 = x0, x_{t+1} = A x_t + B u_t, u_min <= u_t <= u_max, p_min <= C x_t <= p_max,
  *        h . C x_{k+1} + g <= s, s >= 0 for every halfspace (h, g) of step k < min(K, horizon).
  * Solved in the input space (states eliminated) by a primal-dual Mehrotra interior-point method;
- * the halfspace rows enter the Newton system only through per-step 2x2 reductions.
+ * the halfspace rows enter the Newton system only through per-step 2x2 reductions, and each Newton
+ * system is solved by a Riccati recursion over the horizon (no dense Hessian is factored).
  *
  * Conventions as in drcvar_halfspace.h: device pointers unless noted, caller-owned buffers, no
  * allocation or synchronisation inside drcvar_mpc_filter_f64, strides in doubles, DRCVAR_* codes.
@@ -35,7 +36,7 @@
 extern "C" {
 #endif
 
-/* limits of the single-workgroup solver (the condensed Hessian lives in LDS) */
+/* limits of the single-workgroup solver (per-step Riccati factors and input vectors live in LDS) */
 #define DRCVAR_MPC_MAX_STATES 8
 #define DRCVAR_MPC_MAX_INPUTS 4
 #define DRCVAR_MPC_MAX_HORIZON 64

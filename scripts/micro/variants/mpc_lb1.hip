@@ -768,7 +768,7 @@ constexpr int kSweep = 2;
   }
 
 template <int NU, int NMAX, int NX>
-__global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
+__global__ __launch_bounds__(kBlock) void mpc_ipm_kernel(MpcArgs a) {
   extern __shared__ double lds_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;

@@ -142,7 +142,7 @@ def test_model_init_condensation(dyn):
         np.testing.assert_allclose(blob[o:o + size], ref[key].reshape(-1), rtol=1e-12, atol=1e-12,
                                    err_msg=key)
         o += size
-    tail = np.concatenate([A.ravel(), B.ravel(), Q.ravel(), R.ravel()])
+    tail = np.concatenate([A.ravel(), B.ravel(), C.ravel(), Q.ravel(), R.ravel()])
     np.testing.assert_array_equal(blob[o:o + tail.size], tail)
     assert o + tail.size == m.blob_doubles
 
