@@ -161,13 +161,14 @@ struct Lds {
 };
 
 // Fixed LDS plan per size class: every array sits at a compile-time offset, so LDS addresses are
-// immediates and no scalar registers hold array bases.  NMAX = 64 (n <= 64, any H <= 64) or
-// NMAX = 120 (n in 65..120; then nu >= 2, so H <= 60).
+// immediates and no scalar registers hold array bases.  One plan covers every model (n <= NMAX =
+// DRCVAR_MPC_MAX_DECISION, H <= HM = DRCVAR_MPC_MAX_HORIZON): with the Riccati recursion there is
+// no n x n matrix, and the plan stays under 80 KB (two workgroups per CU).
 constexpr int kMx = DRCVAR_MPC_MAX_STATES;  // row stride of the state-dimension matrices in LDS
 constexpr int kMu = DRCVAR_MPC_MAX_INPUTS;
-template <int NMAX>
 struct LdsPlan {
-  static constexpr int HM = NMAX <= 64 ? DRCVAR_MPC_MAX_HORIZON : 60;
+  static constexpr int NMAX = DRCVAR_MPC_MAX_DECISION;
+  static constexpr int HM = DRCVAR_MPC_MAX_HORIZON;
   static constexpr int Am = 0;
   static constexpr int Bm = Am + kMx * kMx;
   static constexpr int Cm = Bm + kMx * kMu;
@@ -202,12 +203,10 @@ struct LdsPlan {
   static constexpr int sc = red + kWaves * kPerStepQ * 64;
   static constexpr int total = sc + 64;
 };
-static_assert(LdsPlan<120>::total * 8 <= 80 * 1024, "plan should allow two workgroups per CU");
-static_assert(LdsPlan<64>::total * 8 <= 80 * 1024, "plan should allow two workgroups per CU");
+static_assert(LdsPlan::total * 8 <= 80 * 1024, "plan should allow two workgroups per CU");
 
-template <int NMAX>
 __device__ inline Lds carve(double* base) {
-  using P = LdsPlan<NMAX>;
+  using P = LdsPlan;
   Lds s;
   s.Am = base + P::Am;
   s.Bm = base + P::Bm;
@@ -374,9 +373,24 @@ __device__ inline double gp_transpose(const Lds& s, const double* z, int j_a, in
 __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 // Inverse of a symmetric positive-definite NU x NU matrix (Gauss-Jordan without pivoting, which is
-// stable for SPD input).  False on a non-positive or non-finite pivot.
+// stable for SPD input; pivot reciprocals by rcp + Newton, ~1 ulp, instead of the long IEEE
+// division sequence on the recursion's critical path).  False on a non-positive or non-finite
+// pivot.
 template <int NU>
 __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[NU][NU]) {
+  if constexpr (NU == 1) {
+    const double piv = a[0][0];
+    inv[0][0] = rcp(piv);
+    return piv > 0.0 && isfinite(piv);
+  } else if constexpr (NU == 2) {  // closed form
+    const double det = a[0][0] * a[1][1] - a[0][1] * a[1][0];
+    const double id = rcp(det);
+    inv[0][0] = a[1][1] * id;
+    inv[1][1] = a[0][0] * id;
+    inv[0][1] = -a[0][1] * id;
+    inv[1][0] = -a[1][0] * id;
+    return a[0][0] > 0.0 && det > 0.0 && isfinite(det) && isfinite(a[0][0]);
+  }
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < NU; ++r)
@@ -386,7 +400,7 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[N
   for (int q = 0; q < NU; ++q) {
     const double piv = a[q][q];
     ok = ok && piv > 0.0 && isfinite(piv);
-    const double ip = 1.0 / piv;
+    const double ip = rcp(piv);
 #pragma unroll
     for (int c = 0; c < NU; ++c) {
       a[q][c] *= ip;
@@ -542,7 +556,7 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 64) {
     const int li = lane < NX ? lane : 0;
-    double Acol[NX], Arow[NX], Bm[NX][NU];
+    double Acol[NX], Arow[NX], Bm[NX][NU], Brow[NU];
 #pragma unroll
     for (int m = 0; m < NX; ++m) {
       Acol[m] = s.Am[m * kMx + li];
@@ -550,27 +564,33 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
 #pragma unroll
       for (int c = 0; c < NU; ++c) Bm[m][c] = s.Bm[m * NU + c];
     }
-    // backward: ge_k = B'p - b_k, kff_k = -Re_k^-1 ge_k (into x), p <- A'p - Kg_k'ge_k
-    double p = 0.0;
-    double kgl[NU], ri[NU][NU], bk[NU];
-    auto load_b = [&](int k) {
+#pragma unroll
+    for (int c = 0; c < NU; ++c) Brow[c] = s.Bm[li * NU + c];
+    // backward: ge_k = B'p - b_k, kff_k = -Re_k^-1 ge_k (into x), p <- A'p - Kg_k'ge_k.
+    // The step data (Kg_k column, Re_k^-1, b_k) are loaded two steps ahead (two register sets,
+    // loop unrolled by two), so no LDS latency sits on the recursion's chain.
+    struct BackStep {
+      double kgl[NU], ri[NU][NU], bk[NU];
+    };
+    auto load_b = [&](BackStep& d, int k) {
+      if (k < 0) return;
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        kgl[c] = s.Kg[(k * NU + c) * kMx + li];
-        bk[c] = x[k * NU + c];
+        d.kgl[c] = s.Kg[(k * NU + c) * kMx + li];
+        d.bk[c] = x[k * NU + c];
 #pragma unroll
-        for (int d = 0; d < NU; ++d) ri[c][d] = s.Ri[(k * NU + c) * NU + d];
+        for (int e = 0; e < NU; ++e) d.ri[c][e] = s.Ri[(k * NU + c) * NU + e];
       }
     };
-    load_b(H - 1);
-    for (int k = H - 1; k >= 0; --k) {
+    double p = 0.0;
+    auto back_step = [&](const BackStep& d, int k) {
       double pv[NX];
 #pragma unroll
       for (int m = 0; m < NX; ++m) pv[m] = readlane_f64(p, m);
       double ge[NU];
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        double acc = -bk[c];
+        double acc = -d.bk[c];
 #pragma unroll
         for (int m = 0; m < NX; ++m) acc += Bm[m][c] * pv[m];
         ge[c] = acc;
@@ -580,40 +600,53 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
       for (int m = 0; m < NX; ++m) np += Acol[m] * pv[m];
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        np -= kgl[c] * ge[c];
+        np -= d.kgl[c] * ge[c];
         double kff = 0.0;
 #pragma unroll
-        for (int d = 0; d < NU; ++d) kff -= ri[c][d] * ge[d];
+        for (int e = 0; e < NU; ++e) kff -= d.ri[c][e] * ge[e];
         mine = lane == c ? kff : mine;
       }
       p = lane < NX ? np : 0.0;
       wave_lds_fence();
-      if (lane < NU) x[k * NU + lane] = mine;  // kff_k
-      if (k > 0) load_b(k - 1);
+      if (lane < NU) x[k * NU + lane] = mine;  // kff_k (b_k was consumed two steps earlier)
+    };
+    {
+      BackStep d0, d1;
+      load_b(d0, H - 1);
+      load_b(d1, H - 2);
+      for (int k = H - 1; k >= 0; k -= 2) {
+        back_step(d0, k);
+        load_b(d0, k - 2);
+        if (k - 1 < 0) break;
+        back_step(d1, k - 1);
+        load_b(d1, k - 3);
+      }
     }
     wave_lds_fence();
-    // forward: du_k = kff_k - Kg_k x_k, x_{k+1} = A x_k + B du_k
-    double kg[NU][NX], ff[NU];
-    auto load_f = [&](int k) {
+    // forward: du_k = kff_k - Kg_k x_k, x_{k+1} = A x_k + B du_k (step data two steps ahead)
+    struct FwdStep {
+      double kg[NU][NX], ff[NU];
+    };
+    auto load_f = [&](FwdStep& d, int k) {
+      if (k >= H) return;
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        ff[c] = x[k * NU + c];
+        d.ff[c] = x[k * NU + c];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) kg[c][m] = s.Kg[(k * NU + c) * kMx + m];
+        for (int m = 0; m < NX; ++m) d.kg[c][m] = s.Kg[(k * NU + c) * kMx + m];
       }
     };
-    load_f(0);
     double xs = 0.0;
-    for (int k = 0; k < H; ++k) {
+    auto fwd_step = [&](const FwdStep& d, int k) {
       double xv[NX];
 #pragma unroll
       for (int m = 0; m < NX; ++m) xv[m] = readlane_f64(xs, m);
       double du[NU], mine = 0.0;
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        double acc = ff[c];
+        double acc = d.ff[c];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) acc -= kg[c][m] * xv[m];
+        for (int m = 0; m < NX; ++m) acc -= d.kg[c][m] * xv[m];
         du[c] = acc;
         mine = lane == c ? acc : mine;
       }
@@ -621,11 +654,22 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
 #pragma unroll
       for (int m = 0; m < NX; ++m) nxs += Arow[m] * xv[m];
 #pragma unroll
-      for (int c = 0; c < NU; ++c) nxs += Bm[li][c] * du[c];
+      for (int c = 0; c < NU; ++c) nxs += Brow[c] * du[c];
       xs = lane < NX ? nxs : 0.0;
       wave_lds_fence();
       if (lane < NU) x[k * NU + lane] = mine;
-      if (k + 1 < H) load_f(k + 1);
+    };
+    {
+      FwdStep d0, d1;
+      load_f(d0, 0);
+      load_f(d1, 1);
+      for (int k = 0; k < H; k += 2) {
+        fwd_step(d0, k);
+        load_f(d0, k + 2);
+        if (k + 1 >= H) break;
+        fwd_step(d1, k + 1);
+        load_f(d1, k + 3);
+      }
     }
   }
   __syncthreads();
@@ -748,7 +792,9 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
 // Row sweep of one thread (lane = halfspace step, obstacles o = wave, wave + 4, ...): the rows
 // of kSweep obstacles are loaded together before any is processed, so kSweep x 8 independent
 // global loads are in flight instead of 8 (the passes are latency-bound at a few hundred rows per
-// thread).  Inside the body: q (the row), o, r (its workspace index).
+// thread).  Deeper sweeps cost registers (two workgroups per CU leave 256 per lane) and measured
+// no faster at C5 (kSweep = 4 with one workgroup per CU: 4.06 vs 4.02 ms).  Inside the body: q
+// (the row), o, r (its workspace index).
 constexpr int kSweep = 2;
 #define ROW_SWEEP_BEGIN                                                              \
   for (int o0_ = wave; o0_ < O; o0_ += kSweep * kWaves) {                            \
@@ -767,13 +813,13 @@ constexpr int kSweep = 2;
   }                   \
   }
 
-template <int NU, int NMAX, int NX>
+template <int NU, int NX>
 __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
   extern __shared__ double lds_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
-  const Lds s = carve<NMAX>(lds_raw);
+  const Lds s = carve(lds_raw);
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + b * a.ws_pp;
 #ifdef DRCVAR_MPC_STAMPS
@@ -1495,18 +1541,18 @@ bool all_finite(const double* p, int64_t n) {
   return true;
 }
 
-template <int NU, int NMAX, int NX>
+template <int NU, int NX>
 int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<NMAX>::total;
+  constexpr size_t lds_bytes = sizeof(double) * LdsPlan::total;
   static bool attr_set = false;  // idempotent; a racing second call sets the same value
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NMAX, NX>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NMAX, NX>), dim3(static_cast<unsigned>(n_problems)),
+  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX>), dim3(static_cast<unsigned>(n_problems)),
                      dim3(kBlock), lds_bytes, stream, args);
   return DRCVAR_OK;
 }
@@ -1514,11 +1560,8 @@ int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
 template <int NU>
 int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
   // state dimension padded to 4 or 8 (the Riccati sweeps are unrolled over it)
-  if (args.nx <= 4)
-    return args.n <= 64 ? launch<NU, 64, 4>(args, n_problems, stream)
-                        : launch<NU, 120, 4>(args, n_problems, stream);
-  return args.n <= 64 ? launch<NU, 64, 8>(args, n_problems, stream)
-                      : launch<NU, 120, 8>(args, n_problems, stream);
+  return args.nx <= 4 ? launch<NU, 4>(args, n_problems, stream)
+                      : launch<NU, 8>(args, n_problems, stream);
 }
 
 }  // namespace
