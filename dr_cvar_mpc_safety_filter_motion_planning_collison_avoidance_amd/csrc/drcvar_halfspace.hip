@@ -50,8 +50,9 @@ constexpr int kStampUnits = 16384, kStamps = 8;
 __device__ unsigned long long g_stamps[kStampUnits * kStamps];
 #define DRCVAR_STAMP(k)                                                                       \
   do {                                                                                        \
-    if (threadIdx.x == 0 && blockIdx.x < kStampUnits)                                         \
-      g_stamps[blockIdx.x * kStamps + (k)] = __builtin_amdgcn_s_memtime();                    \
+    const unsigned su_ = blockIdx.y * gridDim.x + blockIdx.x;                                 \
+    if (threadIdx.x == 0 && su_ < kStampUnits)                                                \
+      g_stamps[su_ * kStamps + (k)] = __builtin_amdgcn_s_memtime();                           \
   } while (0)
 #else
 #define DRCVAR_STAMP(k) \
@@ -217,15 +218,65 @@ __device__ __forceinline__ void block_reduce(double (&v)[K], double* slot) {
   }
 }
 
+// KD fp64 and KF fp32 wave sums at once: the same trees as wave_reduce / wave_sum_f32 (so the
+// results are bitwise those of the one-value forms), written stage by stage across the values so
+// that the independent chains fill each other's DPP hazard slots (one value at a time, the
+// compiler emitted the seven chains back to back: ~750 cycles on the critical path of barrier 1).
+template <int CTRL>
+__device__ __forceinline__ double mov_dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float mov_dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL, int KD, int KF>
+__device__ __forceinline__ void sum_stage(double (&v)[KD], float (&f)[KF]) {
+  double td[KD];
+  float tf[KF];
+#pragma unroll
+  for (int q = 0; q < KD; ++q) td[q] = mov_dpp_f64<CTRL>(v[q]);
+#pragma unroll
+  for (int q = 0; q < KF; ++q) tf[q] = mov_dpp_f32<CTRL>(f[q]);
+#pragma unroll
+  for (int q = 0; q < KD; ++q) v[q] = v[q] + td[q];
+#pragma unroll
+  for (int q = 0; q < KF; ++q) f[q] = f[q] + tf[q];
+}
+template <int KD, int KF>
+__device__ __forceinline__ void wave_sum_multi(double (&v)[KD], float (&f)[KF]) {
+  sum_stage<kDppQuadXor1>(v, f);
+  sum_stage<kDppQuadXor2>(v, f);
+  sum_stage<kDppHalfMirror>(v, f);
+  sum_stage<kDppMirror>(v, f);
+#pragma unroll
+  for (int q = 0; q < KD; ++q) v[q] = swap_combine16<OpAdd>(v[q]);
+#pragma unroll
+  for (int q = 0; q < KF; ++q) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(f[q]), __float_as_int(f[q]), false, false);
+    f[q] = __int_as_float(a[0]) + __int_as_float(a[1]);
+  }
+#pragma unroll
+  for (int q = 0; q < KD; ++q) v[q] = swap_combine32<OpAdd>(v[q]);
+#pragma unroll
+  for (int q = 0; q < KF; ++q) {
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_int(f[q]), __float_as_int(f[q]), false, false);
+    f[q] = __int_as_float(b[0]) + __int_as_float(b[1]);
+  }
+#pragma unroll
+  for (int q = 0; q < KD; ++q) v[q] = uniform_f64(v[q]);
+#pragma unroll
+  for (int q = 0; q < KF; ++q) f[q] = uniform_f32(f[q]);
+}
+
 // Workgroup sums of the load phase: KD fp64 values (the mean sums) and KF fp32 values (the
 // pivot-shifted second moments, which only position the histogram window).  One barrier.
 template <int NW, int KD, int KF>
 __device__ __forceinline__ void block_sum_moments(double (&v)[KD], float (&f)[KF], double* slot_d,
                                                   float* slot_f) {
-#pragma unroll
-  for (int q = 0; q < KD; ++q) v[q] = wave_reduce<OpAdd>(v[q]);
-#pragma unroll
-  for (int q = 0; q < KF; ++q) f[q] = wave_sum_f32(f[q]);
+  wave_sum_multi(v, f);
   if constexpr (NW > 1) {
     const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
@@ -317,16 +368,22 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x, int lane) {
 // Any wave: the bin holding the sample of rank rr (0-based) and the counts below / inside it.
 // Result is uniform across the wave.
 template <int NB>
-__device__ __forceinline__ ScanResult scan_bins(const uint32_t* hist, uint32_t rr, int lane) {
-  constexpr int B = NB / kWave;  // contiguous bins per lane
+__device__ __forceinline__ void load_bins(const uint32_t* hist, int lane, uint32_t (&h)[NB / kWave]) {
+  constexpr int B = NB / kWave;
   const uint32_t* mine = hist + lane * (B + 1);
-  uint32_t h[B];
+#pragma unroll
+  for (int q = 0; q < B; ++q) h[q] = mine[q];
+}
+
+// Same, with this lane's bins already loaded (load_bins) — lets the caller issue the histogram
+// reads together with its other post-barrier LDS reads.
+template <int NB>
+__device__ __forceinline__ ScanResult scan_loaded_bins(const uint32_t (&h)[NB / kWave], uint32_t rr,
+                                                      int lane) {
+  constexpr int B = NB / kWave;  // contiguous bins per lane
   uint32_t s = 0;
 #pragma unroll
-  for (int q = 0; q < B; ++q) {
-    h[q] = mine[q];
-    s += h[q];
-  }
+  for (int q = 0; q < B; ++q) s += h[q];
   const uint32_t incl = wave_inclusive_scan(s, lane);
   const unsigned long long hit = __ballot(incl > rr);
   if (hit == 0ull) return ScanResult{0, 0u, 0u, false};
@@ -349,6 +406,13 @@ __device__ __forceinline__ ScanResult scan_bins(const uint32_t* hist, uint32_t r
                     static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(below), owner)),
                     static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), owner)),
                     true};
+}
+
+template <int NB>
+__device__ __forceinline__ ScanResult scan_bins(const uint32_t* hist, uint32_t rr, int lane) {
+  uint32_t h[NB / kWave];
+  load_bins<NB>(hist, lane, h);
+  return scan_loaded_bins<NB>(h, rr, lane);
 }
 
 __device__ __forceinline__ bool in_range(double d, double lo, double hi) {
@@ -661,9 +725,10 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = tid / kWave;
-  const int64_t u = blockIdx.x;
-  const int64_t o = u / n_steps;
-  const int64_t t = u - o * n_steps;
+  // grid (n_steps, n_obstacles): no integer division ahead of the sample loads (the host splits
+  // launches of more than 65535 obstacles)
+  const int64_t o = blockIdx.y, t = blockIdx.x;
+  const int64_t u = o * n_steps + t;
   const double* base = samples + o * s_obs + t * s_step;
   double* rec = out + u * DRCVAR_OUT_WIDTH;
 
@@ -804,11 +869,13 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     if (lane == 0) wbelow_sh[wave] = wbelow;
     DRCVAR_STAMP(3);
     __syncthreads();                                                      // [barrier 2]
+    uint32_t hb[NB / kWave];  // this lane's bins, read together with the per-wave counts
+    load_bins<NB>(hist, lane, hb);
     uint32_t below = 0;  // all samples below the window
 #pragma unroll
     for (int w = 0; w < NW; ++w) below += wbelow_sh[w];
     if (rank >= below) {
-      const ScanResult sr = scan_bins<NB>(hist, rank - below, lane);     // every wave, same result
+      const ScanResult sr = scan_loaded_bins<NB>(hb, rank - below, lane);  // every wave, same result
       bin = sr.bin;
       rr = rank - below - sr.below;
       c = sr.cnt;
@@ -992,12 +1059,22 @@ struct Launch {
   hipStream_t stream;
 };
 
+// grid (n_steps, obstacles), at most kMaxGridY obstacles per launch (the y-dimension limit):
+// larger batches are split into obstacle chunks on the host
+constexpr int64_t kMaxGridY = 65535;
+
 template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
 void launch_form(const Launch& L) {
-  hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
-                     dim3(static_cast<unsigned>(L.units)), dim3(BLOCK), 0, L.stream, L.samples,
-                     L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp, L.dir,
-                     L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+  const int64_t n_obs = L.units / L.n_steps;
+  for (int64_t o0 = 0; o0 < n_obs; o0 += kMaxGridY) {
+    const int64_t chunk = n_obs - o0 < kMaxGridY ? n_obs - o0 : kMaxGridY;
+    hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
+                       dim3(static_cast<unsigned>(L.n_steps), static_cast<unsigned>(chunk)),
+                       dim3(BLOCK), 0, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
+                       static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
+                       L.dir + o0 * L.dir_s_obs, L.dir_s_obs, L.dir_s_step, L.prm,
+                       L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH);
+  }
 }
 
 template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
@@ -1216,8 +1293,9 @@ int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n
     return DRCVAR_ERR_INVALID_ARGUMENT;
   if (n_units == 0) return DRCVAR_OK;
   if (!samples || !h || !out || n_units > 0x7fffffff) return DRCVAR_ERR_INVALID_ARGUMENT;
-  Launch L{samples, n_units, 1, n_samples, stride_unit, 0, stride_sample,
-           h, h_stride_unit, 0,
+  // units along the grid's x dimension: one "obstacle" of n_units steps
+  Launch L{samples, n_units, n_units, n_samples, 0, stride_unit, stride_sample,
+           h, 0, h_stride_unit,
            make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
            static_cast<hipStream_t>(stream)};
   return dispatch<true>(L, 0, 0);

@@ -226,6 +226,10 @@ def _random_problem(rng, O, T, H, dyn="double", bounds=True, tight=True):
         A = np.eye(4) + 0.01 * rng.normal(size=(4, 4))
         B = 0.2 * rng.normal(size=(4, 3))
         C = np.eye(4)[:2]
+    elif dyn == "generic8":  # the widest state (padded template NX = 8), a dense output map
+        A = np.eye(8) + 0.01 * rng.normal(size=(8, 8))
+        B = 0.2 * rng.normal(size=(8, 2))
+        C = np.eye(8)[:2] + 0.2 * rng.normal(size=(2, 8))
     else:  # generic4
         A = np.eye(5) + 0.01 * rng.normal(size=(5, 5))
         B = 0.2 * rng.normal(size=(5, 4))
@@ -308,7 +312,7 @@ def test_gpu_golden_scenarios_every_metric(path, dev):
     ("double", 7, 5, 12, True, True), ("double", 20, 4, 9, False, True),
     ("double", 25, 0, 0, True, True), ("single", 60, 8, 60, True, True),
     ("generic1", 64, 4, 64, True, True), ("generic3", 40, 5, 40, True, True),
-    ("generic4", 30, 5, 30, True, True),
+    ("generic4", 30, 5, 30, True, True), ("generic8", 24, 4, 24, False, True),
 ])
 def test_gpu_random_problems_match_oracle(dyn, H, O, T, bounds, tight, dev):
     rng = np.random.default_rng(H * 1000 + O * 10 + T)
