@@ -52,8 +52,13 @@ __device__ unsigned long long g_stamps[kStampUnits * kStamps];
   do {                                                                                        \
     const unsigned su_ = blockIdx.y * gridDim.x + blockIdx.x;                                 \
     if (threadIdx.x == 0 && su_ < kStampUnits)                                                \
-      g_stamps[su_ * kStamps + (k)] = __builtin_amdgcn_s_memtime();                           \
+      g_stamps[su_ * kStamps + (k)] = DRCVAR_STAMP_CLOCK();                                   \
   } while (0)
+#ifdef DRCVAR_STAMPS_REALTIME  // 100 MHz clock shared by every XCD: spreads across workgroups
+#define DRCVAR_STAMP_CLOCK() __builtin_amdgcn_s_memrealtime()
+#else  // shader clock of the workgroup's XCD: phase lengths in cycles
+#define DRCVAR_STAMP_CLOCK() __builtin_amdgcn_s_memtime()
+#endif
 #else
 #define DRCVAR_STAMP(k) \
   do {                  \
@@ -488,11 +493,12 @@ __device__ __forceinline__ void append_candidate(double* region, uint32_t& wbase
 // per-wave regions cand[w * kCap + i], i < wcount[w] (global order: wave, then position — fixed).
 // Candidates are pulled into registers (g = lane, lane + 64) and compared through readlane, so
 // the O(c^2) ranking never waits on LDS.  Also returns s_cand = sum over candidates below tau of
-// (cand - tau), accumulated in candidate order.
-template <int NW>
-__device__ __forceinline__ double rank_candidates(const double* cand, const uint32_t* wcount,
-                                                  uint32_t c, uint32_t rr, int lane,
-                                                  double* s_cand) {
+// (cand - tau), accumulated in candidate order.  Q = candidate registers per lane: 1 when
+// c <= 64 (the usual case), 2 up to kCap.
+template <int NW, int Q>
+__device__ __forceinline__ double rank_candidates_q(const double* cand, const uint32_t* wcount,
+                                                    uint32_t c, uint32_t rr, int lane,
+                                                    double* s_cand) {
   const uint32_t cw = lane < NW ? wcount[lane] : 0u;  // lane w < NW: count of wave w
   int slot[2] = {-1, -1};
   uint32_t acc = 0;
@@ -500,7 +506,7 @@ __device__ __forceinline__ double rank_candidates(const double* cand, const uint
   for (int w = 0; w < NW; ++w) {
     const uint32_t nw = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cw), w));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < Q; ++q) {
       const uint32_t g = lane + q * kWave;
       if (g >= acc && g < acc + nw) slot[q] = w * kCap + static_cast<int>(g - acc);
     }
@@ -508,7 +514,7 @@ __device__ __forceinline__ double rank_candidates(const double* cand, const uint
   }
   double mine[2] = {NAN, NAN};  // candidates g = lane, lane + 64
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < Q; ++q)
     if (slot[q] >= 0) mine[q] = cand[slot[q]];
   // per candidate v (lane-parallel): #{z < v}, #{z == v} and sum_{z < v} (z - v); the lane of
   // tau then holds s_cand itself, so no reduction follows the ranking
@@ -518,17 +524,17 @@ __device__ __forceinline__ double rank_candidates(const double* cand, const uint
   for (uint32_t i = 0; i < c0; ++i) {  // uniform trip count
     const double z = readlane_f64(mine[0], static_cast<int>(i));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < Q; ++q) {
       const bool lt = z < mine[q];
       less[q] += lt ? 1u : 0u;
       eq[q] += (z == mine[q]) ? 1u : 0u;
       sl[q] += lt ? z - mine[q] : 0.0;
     }
   }
-  for (uint32_t i = kWave; i < c; ++i) {
+  for (uint32_t i = kWave; Q == 2 && i < c; ++i) {
     const double z = readlane_f64(mine[1], static_cast<int>(i - kWave));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < Q; ++q) {
       const bool lt = z < mine[q];
       less[q] += lt ? 1u : 0u;
       eq[q] += (z == mine[q]) ? 1u : 0u;
@@ -538,7 +544,7 @@ __device__ __forceinline__ double rank_candidates(const double* cand, const uint
   bool found = false;
   double found_v = 0.0, found_s = 0.0;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < Q; ++q) {
     if (lane + q * kWave < c && less[q] <= rr && rr < less[q] + eq[q]) {
       found = true;
       found_v = mine[q];
@@ -549,6 +555,14 @@ __device__ __forceinline__ double rank_candidates(const double* cand, const uint
   const int src = __ffsll(static_cast<long long>(fb)) - 1;
   *s_cand = readlane_f64(found_s, src);
   return readlane_f64(found_v, src);
+}
+template <int NW>
+__device__ __forceinline__ double rank_candidates(const double* cand, const uint32_t* wcount,
+                                                  uint32_t c, uint32_t rr, int lane,
+                                                  double* s_cand) {
+  return c <= static_cast<uint32_t>(kWave)
+             ? rank_candidates_q<NW, 1>(cand, wcount, c, rr, lane, s_cand)
+             : rank_candidates_q<NW, 2>(cand, wcount, c, rr, lane, s_cand);
 }
 
 // Exact selection for the units the register fast path does not finish (degenerate moments, or a
@@ -737,8 +751,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   if (tid == 0) rec[0] = 0.0;  // diagnostic build: dispatch cost only
   return;
 #endif
-#pragma unroll
-  for (int b = tid; b < hist_words<NB>(); b += BLOCK) hist[b] = 0u;
 
   // ---- 1. load + moments ----------------------------------------------------------------
   // Branch-free: idle slots of the last row re-load sample n-1 and contribute zeros.
@@ -769,6 +781,10 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double z_alpha = prm.z_alpha, window_sd = prm.window_sd, hist_scale = prm.hist_scale;
   asm volatile("" ::"s"(e0), "s"(e1), "s"(inv_n), "s"(inv_n0), "s"(deg_sq), "s"(z_alpha),
                "s"(window_sd), "s"(hist_scale));
+  // the histogram is cleared while the sample loads are in flight (barrier 1 orders it before
+  // the first atomic)
+#pragma unroll
+  for (int b = tid; b < hist_words<NB>(); b += BLOCK) hist[b] = 0u;
   // Sums for the mean over every sample (plain sums, as np.mean, in fp64); second moments over
   // row 0 only (the first BLOCK samples), shifted by the unit's first sample and summed in fp32 —
   // they merely position the fast-path window, so a subsample at low precision is enough: an

@@ -38,5 +38,12 @@ print(f"shape {args.shape} geometry {geo}: median unit cycles {np.median(tot):.0
       f"(min {tot.min()}, max {tot.max()})")
 for k, nm in enumerate(names):
     print(f"  {nm:28s} median {np.median(d[:, k]):8.0f} cycles  ({np.median(d[:, k]) / np.median(tot) * 100:5.1f}%)")
-span = st[:, 7].max() - st[:, 0].min()
-print(f"  first entry -> last exit span {span} cycles")
+if os.environ.get("DRCVAR_STAMPS_REALTIME"):  # built with -DDRCVAR_STAMPS_REALTIME: 10 ns ticks
+    t0 = st[:, 0].min()
+    start, end = (st[:, 0] - t0) * 10, (st[:, 7] - t0) * 10
+    q = [0, 10, 50, 90, 100]
+    print("  realtime (ns from the first unit's entry): entry percentiles",
+          np.percentile(start, q).round(), " exit percentiles", np.percentile(end, q).round())
+else:
+    print("  (phase cycles are per-XCD shader clocks; build with -DDRCVAR_STAMPS_REALTIME for the"
+          " spread of entries/exits across workgroups)")
