@@ -159,6 +159,33 @@ def test_bitwise_deterministic():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("O,T", [(65535, 2), (65536, 1), (140_001, 2)])
+def test_obstacle_counts_beyond_one_grid(O, T):
+    """More obstacles than the grid's y dimension holds: the launch is split into obstacle
+    chunks on the host; every unit still lands in its own record."""
+    rng = np.random.default_rng(O + T)
+    N = 24
+    s = rng.normal(size=(O, T, N, 2)) * rng.uniform(0.05, 2.0, size=(O, T, 1, 1))
+    s += rng.uniform(-4, 4, size=(O, 1, 1, 2))
+    e = rng.uniform(-4, 4, size=(T, 2))
+    got = _run(s, e, RiskParams())
+    want = c_oracle.safe_halfspaces(s, e, 0.3, 0.3, 0.2, 0.1, 0.15, nthreads=8)
+    _assert_match(got, want)
+
+
+def test_given_h_many_units():
+    """offsets_given_h puts its units on the grid's x dimension: far beyond 65535 of them."""
+    rng = np.random.default_rng(9)
+    U, N = 200_000, 16
+    s = rng.normal(size=(U, N, 2))
+    h = rng.normal(size=(U, 2))
+    got = engine.offsets_given_h(torch.as_tensor(s).to(DEV), torch.as_tensor(h).to(DEV),
+                                 RiskParams()).cpu().numpy()
+    gc, gs, gt = cf.offsets_given_h(s, h, 0.2, 0.1, 0.15, 0.3, 0.3)
+    np.testing.assert_allclose(got[:, 5], gc, atol=OFFSET_TOL)
+    np.testing.assert_allclose(got[:, 7], gt, atol=OFFSET_TOL)
+
+
 @pytest.mark.parametrize("O,T,N", [(10, 20, 1000), (64, 30, 5000)])
 def test_baseline_configs_vs_c_oracle(O, T, N):
     """BASELINE configs 3 and 4 at full size, every unit checked against the C oracle."""
