@@ -79,6 +79,7 @@ struct Params {
   double inv_k;           // 1 / (alpha N)
   double z_alpha;         // standard-normal alpha-quantile: centre of the fast-path window
   double window_sd;       // half-width of the fast-path window, in sd of d
+  double z_lo;            // z_alpha - window_sd: low edge of the window, in sd of d
   double hist_scale;      // bins / (2 window_sd): bins per sd of d (set per launch plan)
   uint32_t rank;          // min(floor(alpha N), N - 1): 0-based rank of tau
   int unbounded;          // alpha N > N: both LPs unbounded (tau -> -inf), solver-failure sentinel
@@ -661,12 +662,13 @@ __device__ __forceinline__ void select_from_memory(const double* base, int n, in
 }
 
 // compute_separating_vector(ego, mu) (core/geometry.py:35-53): (mu - ego) / |mu - ego|, [1, 0]
-// below 1e-10 (rsqrt + one Newton step; an infinite norm takes the IEEE path as diff / norm does)
+// below 1e-10 (rsqrt + one Newton step).  Branch-free: an overflowing norm (n2 = inf) selects
+// 1/inf = 0, as diff / norm gives 0 (finite diff) or NaN (infinite diff); a NaN n2 stays NaN.
 __device__ __forceinline__ void separating_direction(double mux, double muy, double e0, double e1,
                                                      double deg_sq, double* h0, double* h1) {
   const double dx = mux - e0, dy = muy - e1;
   const double n2 = dx * dx + dy * dy;
-  const double inv = std::isfinite(n2) ? rsqrt_nr(n2) : 1.0 / sqrt(n2);
+  const double inv = n2 == INFINITY ? 0.0 : rsqrt_nr(n2);
   const bool degenerate = n2 < deg_sq;
   *h0 = degenerate ? 1.0 : dx * inv;
   *h1 = degenerate ? 0.0 : dy * inv;
@@ -778,9 +780,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double* dp = dir + o * dir_s_obs + t * dir_s_step;
   const double e0 = dp[0], e1 = dp[1];
   const double inv_n = prm.inv_n, inv_n0 = prm.inv_n0, deg_sq = prm.degenerate_sq;
-  const double z_alpha = prm.z_alpha, window_sd = prm.window_sd, hist_scale = prm.hist_scale;
-  asm volatile("" ::"s"(e0), "s"(e1), "s"(inv_n), "s"(inv_n0), "s"(deg_sq), "s"(z_alpha),
-               "s"(window_sd), "s"(hist_scale));
+  const double z_lo = prm.z_lo, hist_scale = prm.hist_scale;
+  asm volatile("" ::"s"(e0), "s"(e1), "s"(inv_n), "s"(inv_n0), "s"(deg_sq), "s"(z_lo),
+               "s"(hist_scale));
   // the histogram is cleared while the sample loads are in flight (barrier 1 orders it before
   // the first atomic)
 #pragma unroll
@@ -827,10 +829,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   } else {
     separating_direction(mux, muy, e0, e1, deg_sq, &h0, &h1);
   }
-  const double rch = prm.rc * norm_h(h0, h1);  // R_c |h|
   if (bad || prm.unbounded) {  // solver failure, risk_metrics.py:298-303,334-338
     if (tid == 0) {
-      const double r = rch;
+      const double r = prm.rc * norm_h(h0, h1);  // R_c |h|
       double m0, m1, g_mean;
       mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
       store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
@@ -853,7 +854,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // Any positive scale keeps the map monotone, so the approximate reciprocal sqrt is exact enough.
   const double inv_sd = rsqrt_nr(var_d);
   const double sd_d = var_d * inv_sd;
-  const double wlo = mu_d + (z_alpha - window_sd) * sd_d;
+  const double wlo = fma(z_lo, sd_d, mu_d);
   const double scale = prm.hist_scale * inv_sd;
   const LinearMap map{scale, -wlo * scale};
   const uint32_t rank = prm.rank;
@@ -908,6 +909,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 
   // ---- 4. candidates of the target bucket + tail sum below them -----------------------------
   double tau, dsum;  // dsum = sum_{d<tau} (d - tau)
+  double rch;        // R_c |h| (risk_metrics.py:293, :234), wave 0
   if (fast) [[likely]] {
     uint32_t wbase = 0;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -930,6 +932,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
     }
+    rch = prm.rc * norm_h(h0, h1);  // R_c |h|: off the histogram's critical path
     const double s_below = sum_partials<NW>(red_tail);
     double s_cand;
     tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
@@ -942,6 +945,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
     }
+    rch = prm.rc * norm_h(h0, h1);
   }
 
   // ---- 5. offsets (wave 0) -------------------------------------------------------------------
@@ -1201,6 +1205,7 @@ Params make_params(double rr, double ro, double alpha, double delta, double eps,
   const double phi = std::exp(-0.5 * p.z_alpha * p.z_alpha) * 0.3989422804014327;
   const double se = std::sqrt(a * (1.0 - a) / dn) / phi;
   p.window_sd = std::fmax(0.25, 12.0 * se);
+  p.z_lo = p.z_alpha - p.window_sd;
   double t = 1e-20;  // smallest t with sqrt(t) >= 1e-10 (sqrt is correctly rounded and monotone)
   while (std::sqrt(t) >= 1e-10) t = std::nextafter(t, 0.0);
   while (std::sqrt(t) < 1e-10) t = std::nextafter(t, 1.0);
