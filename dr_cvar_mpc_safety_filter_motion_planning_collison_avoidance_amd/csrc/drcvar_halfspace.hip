@@ -593,8 +593,13 @@ __device__ __forceinline__ void select_from_memory(const double* base, int n, in
   block_reduce<OpMin, NW, 1>(vmin, red_rng);
   block_reduce<OpMax, NW, 1>(vmax, red_rng + NW);
   double lo = vmin[0], hi = vmax[0];
+  if (lo == hi) {  // every sample projects to one value (the noise-free step 0): no tail below it
+    *tau_out = lo;
+    *dsum_out = 0.0;
+    return;        // uniform; no second pass over the samples
+  }
   uint32_t rr = rank, c = static_cast<uint32_t>(n);
-  bool have_bin = false, tau_known = lo == hi;
+  bool have_bin = false, tau_known = false;
   double tau = lo;
   int bin = 0;
   BucketMap<LOG_NB> map;
@@ -938,9 +943,34 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
     dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
   } else [[unlikely]] {
-    select_from_memory<BLOCK, LOG_NB, LOAD != kLoadPair>(base, n, s_samp, h0, h1, mu_d, rank,
-                                                         hist, cand, wcount, red_rng, red_tail,
-                                                         &tau, &dsum);
+    // No spread in the moments: the noise-free step 0 of every obstacle (simulation/obstacles.py:63)
+    // has all samples equal — settled from the registers by one min/max reduction (tau = the
+    // common value, no tail below it) instead of the re-reading fallback, which costs two passes
+    // over memory and four barriers and made these units the slowest of a launch.
+    // Small plans only: on the 20-sample plan the extra live range costs the second workgroup
+    // per CU (127 -> 130 VGPRs), and a C5 launch is bandwidth-bound, not set by its slowest unit.
+    bool settled = false;
+    if (P <= 8 && !(var_d > 0.0)) {  // uniform
+      double lo[1] = {INFINITY}, hi[1] = {-INFINITY};
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (tid + j * BLOCK < n) {
+          lo[0] = fmin(lo[0], d[j]);
+          hi[0] = fmax(hi[0], d[j]);
+        }
+      }
+      block_reduce<OpMin, NW, 1>(lo, red_rng);
+      block_reduce<OpMax, NW, 1>(hi, red_rng + NW);
+      if (lo[0] == hi[0]) {  // uniform (the reductions end with identical values in every lane)
+        tau = lo[0];
+        dsum = 0.0;
+        settled = true;
+      }
+    }
+    if (!settled)
+      select_from_memory<BLOCK, LOG_NB, LOAD != kLoadPair>(base, n, s_samp, h0, h1, mu_d, rank,
+                                                           hist, cand, wcount, red_rng, red_tail,
+                                                           &tau, &dsum);
     if (wave != 0) {
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;

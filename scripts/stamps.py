@@ -38,6 +38,9 @@ print(f"shape {args.shape} geometry {geo}: median unit cycles {np.median(tot):.0
       f"(min {tot.min()}, max {tot.max()})")
 for k, nm in enumerate(names):
     print(f"  {nm:28s} median {np.median(d[:, k]):8.0f} cycles  ({np.median(d[:, k]) / np.median(tot) * 100:5.1f}%)")
+slow = np.argsort(tot)[-3:][::-1]
+for u_ in slow:  # where the slowest units (they set the kernel's end) lose their time
+    print(f"  slow unit {u_} (obstacle {u_ // T}, step {u_ % T}): total {tot[u_]}, phases {d[u_].tolist()}")
 if os.environ.get("DRCVAR_STAMPS_REALTIME"):  # built with -DDRCVAR_STAMPS_REALTIME: 10 ns ticks
     t0 = st[:, 0].min()
     start, end = (st[:, 0] - t0) * 10, (st[:, 7] - t0) * 10
