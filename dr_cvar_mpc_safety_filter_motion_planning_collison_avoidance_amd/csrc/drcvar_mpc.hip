@@ -921,36 +921,47 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
   int it = 0, best_it = 0;
   double mu = 0.0, rp = 0.0, rd = 0.0, best_merit = kHuge;
   double* best_u = ws + kRowArrays * pitch;  // [n] best iterate
+  // P1's row part — per-step sums of the weights / duals / affine rhs, the gap and the residual
+  // maxima at positions (p0, p1) — accumulated by each thread for its rows.  It runs fused with
+  // the previous iteration's update pass (P5): the rows are swept once per iteration less.
+  double acc[kPerStepQ], gap_rows, rpm_rows, rdm_rows;
+  auto p1_clear = [&]() {
+#pragma unroll
+    for (int q = 0; q < kPerStepQ; ++q) acc[q] = 0.0;
+    gap_rows = rpm_rows = rdm_rows = 0.0;
+  };
+  auto p1_row = [&](const HsRow& q, double p0, double p1) {
+    const HsLin l = hs_lin(q, p0, p1);
+    const double om = l.DA * (kSlackHess + l.DB) * l.isig;
+    const double rhoA = l.DA * l.rpA - q.lA, rhoB = l.DB * l.rpB - q.lB;
+    const double coef = rhoA - l.DA * (-l.rds + rhoA + rhoB) * l.isig;
+    acc[0] += q.lA * q.h0;
+    acc[1] += q.lA * q.h1;
+    acc[2] += om * q.h0 * q.h0;
+    acc[3] += om * q.h0 * q.h1;
+    acc[4] += om * q.h1 * q.h1;
+    acc[5] += coef * q.h0;
+    acc[6] += coef * q.h1;
+    gap_rows += q.wA * q.lA + q.wB * q.lB;
+    rpm_rows = fmax(rpm_rows, fmax(fabs(l.rpA), fabs(l.rpB)));
+    rdm_rows = fmax(rdm_rows, fabs(l.rds));
+  };
+  // positions of the starting iterate and its P1 row pass
+  positions<NU>(s, s.u, s.p, s.c, H);
+  __syncthreads();
+  p1_clear();
+  if (lane < K) {
+    const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+    ROW_SWEEP_BEGIN
+      p1_row(q, p0, p1);
+    ROW_SWEEP_END
+  }
   for (it = 1; it <= a.max_iter; ++it) {
-    // ---- positions of the iterate ----
     MPC_PHASE(15);
-    positions<NU>(s, s.u, s.p, s.c, H);
-    __syncthreads();
-    MPC_PHASE(14);
 
-    // ---- P1: residuals, weights, per-step S / v / affine rhs ----
+    // ---- P1: residuals, weights, per-step S / v / affine rhs (row sums already taken) ----
     {
-      double acc[kPerStepQ] = {0, 0, 0, 0, 0, 0, 0};
-      double gap = 0.0, rpm = 0.0, rdm = 0.0;
-      if (lane < K) {
-        const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-        ROW_SWEEP_BEGIN
-          const HsLin l = hs_lin(q, p0, p1);
-          const double om = l.DA * (kSlackHess + l.DB) * l.isig;
-          const double rhoA = l.DA * l.rpA - q.lA, rhoB = l.DB * l.rpB - q.lB;
-          const double coef = rhoA - l.DA * (-l.rds + rhoA + rhoB) * l.isig;
-          acc[0] += q.lA * q.h0;
-          acc[1] += q.lA * q.h1;
-          acc[2] += om * q.h0 * q.h0;
-          acc[3] += om * q.h0 * q.h1;
-          acc[4] += om * q.h1 * q.h1;
-          acc[5] += coef * q.h0;
-          acc[6] += coef * q.h1;
-          gap += q.wA * q.lA + q.wB * q.lB;
-          rpm = fmax(rpm, fmax(fabs(l.rpA), fabs(l.rpB)));
-          rdm = fmax(rdm, fabs(l.rds));
-        ROW_SWEEP_END
-      }
+      double gap = gap_rows, rpm = rpm_rows, rdm = rdm_rows;
 #pragma unroll
       for (int q = 0; q < kPerStepQ; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
       __syncthreads();
@@ -1180,20 +1191,16 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     }
     const double alpha = fmin(1.0, kStepFrac * block_min(amax, s.sc));
 
-    // ---- P5: update ----
+    // ---- P5: update (the halfspace rows in the fused pass below) ----
+    // this lane's step: positions and directions of the iterate being updated
+    double p0 = 0.0, p1 = 0.0, a0 = 0.0, a1 = 0.0, d0 = 0.0, d1 = 0.0;
     if (lane < K) {
-      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-      const double a0 = s.dpa[2 * lane], a1 = s.dpa[2 * lane + 1];
-      const double d0 = s.dp[2 * lane], d1 = s.dp[2 * lane + 1];
-      ROW_SWEEP_BEGIN
-        const HsLin l = hs_lin(q, p0, p1);
-        const RowDir d = hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu);
-        rows.s[r] = q.sv + alpha * d.ds;
-        rows.wA[r] = q.wA + alpha * d.dwA;
-        rows.lA[r] = q.lA + alpha * d.dlA;
-        rows.wB[r] = q.wB + alpha * d.dwB;
-        rows.lB[r] = q.lB + alpha * d.dlB;
-      ROW_SWEEP_END
+      p0 = s.p[2 * lane];
+      p1 = s.p[2 * lane + 1];
+      a0 = s.dpa[2 * lane];
+      a1 = s.dpa[2 * lane + 1];
+      d0 = s.dp[2 * lane];
+      d1 = s.dp[2 * lane + 1];
     }
     // box / position rows: every thread reads its own entries only, so no barrier is needed
     // between computing the direction and writing the update
@@ -1224,6 +1231,31 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     __syncthreads();  // positions of the box loop read s.u; update it only after every reader
     for (int j = tid; j < n; j += kBlock) s.u[j] += alpha * s.du[j];
     __syncthreads();
+    MPC_PHASE(5);
+    positions<NU>(s, s.u, s.p, s.c, H);  // of the updated iterate (next iteration's P1)
+    __syncthreads();
+    MPC_PHASE(14);
+    // fused pass: each halfspace row is updated (P5) and enters the next iteration's P1 sums
+    p1_clear();
+    if (lane < K) {
+      const double pn0 = s.p[2 * lane], pn1 = s.p[2 * lane + 1];
+      ROW_SWEEP_BEGIN
+        const HsLin l = hs_lin(q, p0, p1);
+        const RowDir d = hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu);
+        HsRow qn = q;
+        qn.sv = q.sv + alpha * d.ds;
+        qn.wA = q.wA + alpha * d.dwA;
+        qn.lA = q.lA + alpha * d.dlA;
+        qn.wB = q.wB + alpha * d.dwB;
+        qn.lB = q.lB + alpha * d.dlB;
+        rows.s[r] = qn.sv;
+        rows.wA[r] = qn.wA;
+        rows.lA[r] = qn.lA;
+        rows.wB[r] = qn.wB;
+        rows.lB[r] = qn.lB;
+        p1_row(qn, pn0, pn1);
+      ROW_SWEEP_END
+    }
     MPC_PHASE(5);
   }
   if (it > a.max_iter) it = a.max_iter;
