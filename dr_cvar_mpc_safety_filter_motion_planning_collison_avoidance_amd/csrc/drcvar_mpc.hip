@@ -42,8 +42,12 @@
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
+// Threads per problem: 256 for batches (two workgroups per CU), 512 for launches of a few
+// problems (two waves per SIMD hide the row passes' fp64 latency; the chip has CUs to spare).
+// Device code below is written against kBlock / kWaves, which the kernel defines from its
+// BLK parameter; helpers take the wave count as a template argument.
+constexpr int kMaxWaves = 8;
+constexpr int kFewProblems = 128;  // at most this many problems per launch: 512-thread form
 constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
 constexpr int kRowArrays = 8; // h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
 constexpr int kBestPad = 128; // best iterate u (n <= DRCVAR_MPC_MAX_DECISION)
@@ -166,6 +170,7 @@ struct Lds {
 // no n x n matrix, and the plan stays under 80 KB (two workgroups per CU).
 constexpr int kMx = DRCVAR_MPC_MAX_STATES;  // row stride of the state-dimension matrices in LDS
 constexpr int kMu = DRCVAR_MPC_MAX_INPUTS;
+template <int NW>  // waves per workgroup (sizes the per-step partial sums)
 struct LdsPlan {
   static constexpr int NMAX = DRCVAR_MPC_MAX_DECISION;
   static constexpr int HM = DRCVAR_MPC_MAX_HORIZON;
@@ -200,13 +205,15 @@ struct LdsPlan {
   static constexpr int Mp = S + 3 * HM;
   static constexpr int xs = Mp + 2 * DRCVAR_MPC_MAX_INPUTS * HM;
   static constexpr int red = xs + (HM + 1) * DRCVAR_MPC_MAX_STATES;
-  static constexpr int sc = red + kWaves * kPerStepQ * 64;
+  static constexpr int sc = red + NW * kPerStepQ * 64;
   static constexpr int total = sc + 64;
 };
-static_assert(LdsPlan::total * 8 <= 80 * 1024, "plan should allow two workgroups per CU");
+static_assert(LdsPlan<4>::total * 8 <= 80 * 1024, "256-thread plan: two workgroups per CU");
+static_assert(LdsPlan<8>::total * 8 <= 160 * 1024, "512-thread plan exceeds the LDS");
 
+template <int NW>
 __device__ inline Lds carve(double* base) {
-  using P = LdsPlan;
+  using P = LdsPlan<NW>;
   Lds s;
   s.Am = base + P::Am;
   s.Bm = base + P::Bm;
@@ -261,6 +268,7 @@ __device__ __forceinline__ double wave_min(double v) {
 }
 
 // Three block-wide reductions (sum, max, max) in one LDS round trip; waves combined in order.
+template <int kWaves>
 __device__ inline void block_sum_max_max(double& a, double& b, double& c, double* sc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   a = wave_sum(a);
@@ -284,6 +292,7 @@ __device__ inline void block_sum_max_max(double& a, double& b, double& c, double
   __syncthreads();
 }
 
+template <int kWaves>
 __device__ inline double block_min(double a, double* sc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   a = wave_min(a);
@@ -296,6 +305,7 @@ __device__ inline double block_min(double a, double* sc) {
   return r;
 }
 
+template <int kWaves>
 __device__ inline double block_sum(double a, double* sc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   a = wave_sum(a);
@@ -327,7 +337,7 @@ __device__ __forceinline__ double ratio(double x, double dx) {
 }
 
 // p[2k+i] = c[2k+i] + sum_{j<=k} Mp[k-j][i][:] . u[j*nu : (j+1)*nu]
-template <int NU>
+template <int NU, int kBlock>
 __device__ inline void positions(const Lds& s, const double* u, double* out, const double* c, int H) {
   for (int t = threadIdx.x; t < 2 * H; t += kBlock) {
     const int k = t >> 1, i = t & 1;
@@ -782,6 +792,7 @@ __device__ __forceinline__ PairState pos_state(const Lds& s, int H, int t) {
 }
 
 // Sum kWaves per-step partials (wave 0, lane = step) in wave order.
+template <int kWaves>
 __device__ __forceinline__ double step_total(const double* red, int q, int lane) {
   double t = red[q * 64 + lane];
 #pragma unroll
@@ -813,13 +824,16 @@ constexpr int kSweep = 2;
   }                   \
   }
 
-template <int NU, int NX>
-__global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
+template <int NU, int NX, int BLK>
+__global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
+  constexpr int kBlock = BLK;
+  constexpr int kWaves = BLK / 64;
+  static_assert(kWaves <= kMaxWaves, "LDS plan sized for kMaxWaves");
   extern __shared__ double lds_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
-  const Lds s = carve(lds_raw);
+  const Lds s = carve<kWaves>(lds_raw);
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + b * a.ws_pp;
 #ifdef DRCVAR_MPC_STAMPS
@@ -910,7 +924,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
   for (int j = tid; j < n; j += kBlock) fmaxv = fmax(fmaxv, fabs(s.f[j]));
   {
     double unused = 0.0;
-    block_sum_max_max(unused, gmax, fmaxv, s.sc);
+    block_sum_max_max<kWaves>(unused, gmax, fmaxv, s.sc);
   }
   const double scale_d = 1.0 + gmax;
   const double scale_q = 1.0 + fmax(fmaxv, kSlackLin);
@@ -947,7 +961,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     rdm_rows = fmax(rdm_rows, fabs(l.rds));
   };
   // positions of the starting iterate and its P1 row pass
-  positions<NU>(s, s.u, s.p, s.c, H);
+  positions<NU, kBlock>(s, s.u, s.p, s.c, H);
   __syncthreads();
   p1_clear();
   if (lane < K) {
@@ -968,7 +982,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
       if (wave == 0 && lane < H) {
         double tot[kPerStepQ];
 #pragma unroll
-        for (int q = 0; q < kPerStepQ; ++q) tot[q] = lane < K ? step_total(s.red, q, lane) : 0.0;
+        for (int q = 0; q < kPerStepQ; ++q) tot[q] = lane < K ? step_total<kWaves>(s.red, q, lane) : 0.0;
         if (a.has_p) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -1014,7 +1028,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
         s.rdu[j] = r;
         rdm = fmax(rdm, fabs(r));
       }
-      block_sum_max_max(gap, rpm, rdm, s.sc);
+      block_sum_max_max<kWaves>(gap, rpm, rdm, s.sc);
       mu = m_ineq > 0.0 ? gap / m_ineq : 0.0;
       rp = rpm;
       rd = rdm;
@@ -1049,7 +1063,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     MPC_PHASE(3);
     riccati_solve<NU, NX>(s, H, s.dua);
     MPC_PHASE(4);
-    positions<NU>(s, s.dua, s.dpa, nullptr, H);
+    positions<NU, kBlock>(s, s.dua, s.dpa, nullptr, H);
     __syncthreads();
     MPC_PHASE(14);
 
@@ -1079,7 +1093,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
         amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dpa[t], 0.0, false)));
       }
     }
-    const double a_aff = fmin(1.0, block_min(amax, s.sc));
+    const double a_aff = fmin(1.0, block_min<kWaves>(amax, s.sc));
 
     // ---- P3: affine gap and the corrector rhs as base + sigma*mu * unit ----
     {
@@ -1109,7 +1123,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
       if (wave == 0 && lane < H) {
         double tot[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tot[q] = lane < K ? step_total(s.red, q, lane) : 0.0;
+        for (int q = 0; q < 4; ++q) tot[q] = lane < K ? step_total<kWaves>(s.red, q, lane) : 0.0;
         if (a.has_p) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -1145,7 +1159,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
           s.rUu[j] = 0.0;
         }
       }
-      gap_aff = block_sum(gap_aff, s.sc);  // its barriers also publish za / zu / rU / rUu
+      gap_aff = block_sum<kWaves>(gap_aff, s.sc);  // its barriers also publish za / zu / rU / rUu
       const double ratio_g = gap > 0.0 ? gap_aff / gap : 0.0;
       const double sigma_mu = ratio_g * ratio_g * ratio_g * mu;
       s.sc[63] = sigma_mu;  // same value in every thread; kept for P4/P5
@@ -1158,7 +1172,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     MPC_PHASE(5);
     riccati_solve<NU, NX>(s, H, s.du);
     MPC_PHASE(4);
-    positions<NU>(s, s.du, s.dp, nullptr, H);
+    positions<NU, kBlock>(s, s.du, s.dp, nullptr, H);
     __syncthreads();
     MPC_PHASE(14);
 
@@ -1189,7 +1203,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
         amax = fmin(amax, pair_ratio(q, pair_dir(q, l, s.dpa[t], s.dp[t], sigma_mu, true)));
       }
     }
-    const double alpha = fmin(1.0, kStepFrac * block_min(amax, s.sc));
+    const double alpha = fmin(1.0, kStepFrac * block_min<kWaves>(amax, s.sc));
 
     // ---- P5: update (the halfspace rows in the fused pass below) ----
     // this lane's step: positions and directions of the iterate being updated
@@ -1232,7 +1246,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     for (int j = tid; j < n; j += kBlock) s.u[j] += alpha * s.du[j];
     __syncthreads();
     MPC_PHASE(5);
-    positions<NU>(s, s.u, s.p, s.c, H);  // of the updated iterate (next iteration's P1)
+    positions<NU, kBlock>(s, s.u, s.p, s.c, H);  // of the updated iterate (next iteration's P1)
     __syncthreads();
     MPC_PHASE(14);
     // fused pass: each halfspace row is updated (P5) and enters the next iteration's P1 sums
@@ -1331,9 +1345,9 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
         for (int q = 0; q < 3; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
         __syncthreads();
         if (wave == 0 && lane < H) {
-          double t0 = lane < K ? step_total(s.red, 0, lane) : 0.0;
-          const double t1 = lane < K ? step_total(s.red, 1, lane) : 0.0;
-          double t2 = lane < K ? step_total(s.red, 2, lane) : 0.0;
+          double t0 = lane < K ? step_total<kWaves>(s.red, 0, lane) : 0.0;
+          const double t1 = lane < K ? step_total<kWaves>(s.red, 1, lane) : 0.0;
+          double t2 = lane < K ? step_total<kWaves>(s.red, 2, lane) : 0.0;
           if (a.has_p) {
             t0 += kPolishRho * (s.px[2 * lane] + s.px[4 * H + 2 * lane]);
             t2 += kPolishRho * (s.px[2 * lane + 1] + s.px[4 * H + 2 * lane + 1]);
@@ -1372,7 +1386,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const int t = 2 * lane + i;
-            double z = lane < K ? step_total(s.red, i, lane) : 0.0;
+            double z = lane < K ? step_total<kWaves>(s.red, i, lane) : 0.0;
             if (a.has_p) {
               if (s.px[t] != 0.0) z += s.px[2 * H + t] - kPolishRho * (a.pmax[i] - s.c[t]);
               if (s.px[4 * H + t] != 0.0) z -= s.px[6 * H + t] - kPolishRho * (s.c[t] - a.pmin[i]);
@@ -1395,7 +1409,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
         riccati_solve<NU, NX>(s, H, s.du);
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
-        positions<NU>(s, s.u, s.p, s.c, H);
+        positions<NU, kBlock>(s, s.u, s.p, s.c, H);
         __syncthreads();
         MPC_PHASE(13);
         // multiplier updates nu += rho * (E u - e)
@@ -1474,7 +1488,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
           }
         }
       }
-      bad = block_sum(bad, s.sc);
+      bad = block_sum<kWaves>(bad, s.sc);
       if (bad == 0.0) polished = true;
     }
     if (polished) {
@@ -1494,7 +1508,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
   }
   for (int q = tid; q < nx; q += kBlock) s.xs[q] = x0[q];
   __syncthreads();
-  positions<NU>(s, s.u, s.p, s.c, H);  // positions of the returned inputs (slacks below)
+  positions<NU, kBlock>(s, s.u, s.p, s.c, H);  // positions of the returned inputs (slacks below)
   const double* A = a.blob + a.off.A;
   const double* B = a.blob + a.off.B;
   for (int t = 0; t < H; ++t) {  // x_{t+1} = A x_t + B u_t (core/mpc_filter.py:85-86, :216-217)
@@ -1538,7 +1552,7 @@ __global__ __launch_bounds__(kBlock, 2) void mpc_ipm_kernel(MpcArgs a) {
     }
   }
   double unused = 0.0;
-  block_sum_max_max(obj, smax, unused, s.sc);
+  block_sum_max_max<kWaves>(obj, smax, unused, s.sc);
   double* xo = a.x_out + b * (H + 1) * nx;
   for (int q = tid; q < (H + 1) * nx; q += kBlock) xo[q] = s.xs[q];
   double* uo = a.u_out + b * n;
@@ -1573,27 +1587,32 @@ bool all_finite(const double* p, int64_t n) {
   return true;
 }
 
-template <int NU, int NX>
+template <int NU, int NX, int BLK>
 int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  constexpr size_t lds_bytes = sizeof(double) * LdsPlan::total;
+  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<BLK / 64>::total;
   static bool attr_set = false;  // idempotent; a racing second call sets the same value
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX>), dim3(static_cast<unsigned>(n_problems)),
-                     dim3(kBlock), lds_bytes, stream, args);
+  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK>), dim3(static_cast<unsigned>(n_problems)),
+                     dim3(BLK), lds_bytes, stream, args);
   return DRCVAR_OK;
 }
 
 template <int NU>
 int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  // state dimension padded to 4 or 8 (the Riccati sweeps are unrolled over it)
-  return args.nx <= 4 ? launch<NU, 4>(args, n_problems, stream)
-                      : launch<NU, 8>(args, n_problems, stream);
+  // state dimension padded to 4 or 8 (the Riccati sweeps are unrolled over it); a launch of a
+  // few problems cannot fill the chip, so each problem gets 512 threads
+  const bool few = n_problems <= kFewProblems;
+  if (args.nx <= 4)
+    return few ? launch<NU, 4, 512>(args, n_problems, stream)
+               : launch<NU, 4, 256>(args, n_problems, stream);
+  return few ? launch<NU, 8, 512>(args, n_problems, stream)
+             : launch<NU, 8, 256>(args, n_problems, stream);
 }
 
 }  // namespace
