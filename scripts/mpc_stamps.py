@@ -13,9 +13,9 @@ from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _na
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf  # noqa: E402
 from mpc_bench import problem_batch  # noqa: E402
 
-NAMES = {0: "setup", 1: "P1 residuals+weights", 2: "assemble K", 3: "cholesky (ipm)",
-         4: "triangular solves (ipm)", 5: "row passes P2-P5", 6: "loop exit", 7: "polish other",
-         8: "output", 10: "polish classify+assemble", 11: "polish cholesky",
+NAMES = {0: "setup", 1: "P1 residuals+weights", 2: "affine rhs", 3: "Riccati factor (ipm)",
+         4: "Riccati solves (ipm)", 5: "row passes P2-P5", 6: "loop exit", 7: "polish other",
+         8: "output", 10: "polish classify+assemble", 11: "polish Riccati factor",
          12: "polish row passes", 13: "polish solves", 14: "positions (ipm)", 15: "loop top"}
 dev = torch.device("cuda", 0)
 lib = _native.lib()
