@@ -138,8 +138,10 @@ struct Lds {
   double* P;      // [nx][kMx] Riccati cost-to-go
   double* T;      // [nx][kMx] P A
   double* U;      // [nx][NU] P B
-  double* Kg;     // [H][NU][kMx] feedback gains Re^-1 B'PA
+  double* Kg;     // [H][NU][NX] feedback gains Re^-1 B'PA
   double* Ri;     // [H][NU][NU] Re^-1
+  double* SM;     // [H][NX][NX] parallel-scan maps (NX <= 4)
+  double* SV;     // [H][NX] parallel-scan offsets (NX <= 4)
   double* u;      // [n] inputs (the iterate)
   double* dua;    // [n] affine direction
   double* du;     // [n] corrector direction
@@ -170,7 +172,9 @@ struct Lds {
 // no n x n matrix, and the plan stays under 80 KB (two workgroups per CU).
 constexpr int kMx = DRCVAR_MPC_MAX_STATES;  // row stride of the state-dimension matrices in LDS
 constexpr int kMu = DRCVAR_MPC_MAX_INPUTS;
-template <int NW>  // waves per workgroup (sizes the per-step partial sums)
+// NW waves per workgroup (the per-step partial sums), NU inputs and NX (padded) states (the
+// per-step Riccati factors and, for NX <= 4, the parallel-scan buffers)
+template <int NW, int NU, int NX>
 struct LdsPlan {
   static constexpr int NMAX = DRCVAR_MPC_MAX_DECISION;
   static constexpr int HM = DRCVAR_MPC_MAX_HORIZON;
@@ -183,8 +187,10 @@ struct LdsPlan {
   static constexpr int T = P + kMx * kMx;
   static constexpr int U = T + kMx * kMx;
   static constexpr int Kg = U + kMx * kMu;
-  static constexpr int Ri = Kg + HM * kMu * kMx;
-  static constexpr int u = Ri + HM * kMu * kMu;
+  static constexpr int Ri = Kg + HM * NU * NX;
+  static constexpr int SM = Ri + HM * NU * NU;                   // scan: [HM][NX][NX] maps
+  static constexpr int SV = SM + (NX <= 4 ? HM * NX * NX : 0);   // scan: [HM][NX] offsets
+  static constexpr int u = SV + (NX <= 4 ? HM * NX : 0);
   static constexpr int dua = u + NMAX;
   static constexpr int du = dua + NMAX;
   static constexpr int rdu = du + NMAX;
@@ -208,12 +214,13 @@ struct LdsPlan {
   static constexpr int sc = red + NW * kPerStepQ * 64;
   static constexpr int total = sc + 64;
 };
-static_assert(LdsPlan<4>::total * 8 <= 80 * 1024, "256-thread plan: two workgroups per CU");
-static_assert(LdsPlan<8>::total * 8 <= 160 * 1024, "512-thread plan exceeds the LDS");
+static_assert(LdsPlan<4, 4, 4>::total * 8 <= 80 * 1024, "256-thread plan: two workgroups per CU");
+static_assert(LdsPlan<4, 4, 8>::total * 8 <= 80 * 1024, "256-thread plan: two workgroups per CU");
+static_assert(LdsPlan<8, 4, 8>::total * 8 <= 160 * 1024, "512-thread plan exceeds the LDS");
 
-template <int NW>
+template <int NW, int NU, int NX>
 __device__ inline Lds carve(double* base) {
-  using P = LdsPlan<NW>;
+  using P = LdsPlan<NW, NU, NX>;
   Lds s;
   s.Am = base + P::Am;
   s.Bm = base + P::Bm;
@@ -225,6 +232,8 @@ __device__ inline Lds carve(double* base) {
   s.U = base + P::U;
   s.Kg = base + P::Kg;
   s.Ri = base + P::Ri;
+  s.SM = base + P::SM;
+  s.SV = base + P::SV;
   s.u = base + P::u;
   s.dua = base + P::dua;
   s.du = base + P::du;
@@ -534,7 +543,7 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
       }
       if (lane < NX2 && i == j) {
 #pragma unroll
-        for (int c = 0; c < NU; ++c) s.Kg[(k * NU + c) * kMx + j] = Kj[c];
+        for (int c = 0; c < NU; ++c) s.Kg[(k * NU + c) * NX + j] = Kj[c];
       }
       if (lane < NX2 && k > 0 && i >= j) {
         double acc = qnext;
@@ -586,7 +595,7 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
       if (k < 0) return;
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        d.kgl[c] = s.Kg[(k * NU + c) * kMx + li];
+        d.kgl[c] = s.Kg[(k * NU + c) * NX + li];
         d.bk[c] = x[k * NU + c];
 #pragma unroll
         for (int e = 0; e < NU; ++e) d.ri[c][e] = s.Ri[(k * NU + c) * NU + e];
@@ -643,7 +652,7 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
       for (int c = 0; c < NU; ++c) {
         d.ff[c] = x[k * NU + c];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) d.kg[c][m] = s.Kg[(k * NU + c) * kMx + m];
+        for (int m = 0; m < NX; ++m) d.kg[c][m] = s.Kg[(k * NU + c) * NX + m];
       }
     };
     double xs = 0.0;
@@ -683,6 +692,132 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
     }
   }
   __syncthreads();
+}
+
+// Parallel-scan form of riccati_solve for NX <= 4 (the reference's double integrator and every
+// smaller model).  Both passes are affine recurrences in the state dimension,
+//   backward  p_k = F_k p_{k+1} + Kg_k' b_k       (p_H = 0),   F_k = A' - Kg_k' B'
+//   forward   x_{k+1} = F_k' x_k + B kff_k         (x_0 = 0),   kff_k = -Re_k^-1 (B' p_{k+1} - b_k)
+// so each is a Hillis-Steele scan of affine maps (M, v) over the horizon — ceil(log2 H) levels,
+// each composing every map with its partner d steps away (M_k <- M_k M_k', v_k <- M_k v_k' + v_k)
+// in place, operands read before a barrier — instead of H dependent steps on one wave.  Thread
+// (k, i) owns row i of map k (H * NX <= 256 threads).  Then kff_k and du_k are per step.
+template <int NX, int kBlock>
+__device__ inline void scan_maps(double* M, double* V, int H, int dir) {
+  const int t = threadIdx.x, k = t / NX, i = t - (t / NX) * NX;
+  const bool own = t < H * NX;
+  for (int d = 1; d < H; d <<= 1) {
+    const int kp = k + dir * d;
+    double row[NX], vi = 0.0;
+    if (own) {
+      const double* mk = M + (k * NX + i) * NX;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) row[j] = mk[j];
+      vi = V[k * NX + i];
+      if (kp >= 0 && kp < H) {
+        const double* mp = M + kp * NX * NX;
+        const double* vp = V + kp * NX;
+        double nr[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          double acc = 0.0;
+#pragma unroll
+          for (int m = 0; m < NX; ++m) acc += row[m] * mp[m * NX + j];
+          nr[j] = acc;
+        }
+#pragma unroll
+        for (int m = 0; m < NX; ++m) vi += row[m] * vp[m];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) row[j] = nr[j];
+      }
+    }
+    __syncthreads();
+    if (own) {
+      double* mk = M + (k * NX + i) * NX;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) mk[j] = row[j];
+      V[k * NX + i] = vi;
+    }
+    __syncthreads();
+  }
+}
+
+template <int NU, int NX, int kBlock>
+__device__ inline void riccati_solve_scan(const Lds& s, int H, double* x) {
+  static_assert(NX <= 4 && DRCVAR_MPC_MAX_HORIZON * 4 <= kBlock, "one thread per map row");
+  const int t = threadIdx.x, k = t / NX, i = t - (t / NX) * NX;
+  const bool own = t < H * NX;
+  double* M = s.SM;
+  double* V = s.SV;
+  // F_k[r][c] = A[c][r] - sum_u Kg_k[u][r] B[c][u]
+  auto F = [&](int kk, int r, int c) {
+    double acc = s.Am[c * kMx + r];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc -= s.Kg[(kk * NU + u) * NX + r] * s.Bm[c * NU + u];
+    return acc;
+  };
+  // ---- backward: maps (F_k, Kg_k' b_k), suffix scan; p_k = V_k
+  if (own) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) M[(k * NX + i) * NX + j] = F(k, i, j);
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc += s.Kg[(k * NU + u) * NX + i] * x[k * NU + u];
+    V[k * NX + i] = acc;
+  }
+  __syncthreads();
+  scan_maps<NX, kBlock>(M, V, H, +1);
+  // kff_k = -Re_k^-1 (B' p_{k+1} - b_k), thread (k, u) for u < NU
+  double kff = 0.0;
+  const bool ownu = t < H * NU;
+  const int ku = t / NU, uu = t - (t / NU) * NU;
+  if (ownu) {
+#pragma unroll
+    for (int e = 0; e < NU; ++e) {
+      double ge = -x[ku * NU + e];
+      if (ku + 1 < H) {
+#pragma unroll
+        for (int m = 0; m < NX; ++m) ge += s.Bm[m * NU + e] * V[(ku + 1) * NX + m];
+      }
+      kff -= s.Ri[(ku * NU + uu) * NU + e] * ge;
+    }
+  }
+  __syncthreads();
+  if (ownu) x[ku * NU + uu] = kff;
+  __syncthreads();
+  // ---- forward: maps (F_k', B kff_k), prefix scan; x_{k+1} = V_k
+  if (own) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) M[(k * NX + i) * NX + j] = F(k, j, i);
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc += s.Bm[i * NU + u] * x[k * NU + u];
+    V[k * NX + i] = acc;
+  }
+  __syncthreads();
+  scan_maps<NX, kBlock>(M, V, H, -1);
+  // du_k = kff_k - Kg_k x_k, x_k = V_{k-1} (x_0 = 0)
+  double du = 0.0;
+  if (ownu) {
+    du = x[ku * NU + uu];
+    if (ku > 0) {
+#pragma unroll
+      for (int m = 0; m < NX; ++m) du -= s.Kg[(ku * NU + uu) * NX + m] * V[(ku - 1) * NX + m];
+    }
+  }
+  __syncthreads();
+  if (ownu) x[ku * NU + uu] = du;
+  __syncthreads();
+}
+
+// K x = b: the parallel scan for NX <= 4, the wave-serial recursion otherwise
+template <int NU, int NX, int kBlock>
+__device__ inline void newton_solve(const Lds& s, int H, double* x) {
+  if constexpr (NX <= 4) {
+    riccati_solve_scan<NU, NX, kBlock>(s, H, x);
+  } else {
+    riccati_solve<NU, NX>(s, H, x);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -833,7 +968,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
-  const Lds s = carve<kWaves>(lds_raw);
+  const Lds s = carve<kWaves, NU, NX>(lds_raw);
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + b * a.ws_pp;
 #ifdef DRCVAR_MPC_STAMPS
@@ -1061,7 +1196,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
       break;
     }
     MPC_PHASE(3);
-    riccati_solve<NU, NX>(s, H, s.dua);
+    newton_solve<NU, NX, kBlock>(s, H, s.dua);
     MPC_PHASE(4);
     positions<NU, kBlock>(s, s.dua, s.dpa, nullptr, H);
     __syncthreads();
@@ -1170,7 +1305,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     }
     const double sigma_mu = s.sc[63];
     MPC_PHASE(5);
-    riccati_solve<NU, NX>(s, H, s.du);
+    newton_solve<NU, NX, kBlock>(s, H, s.du);
     MPC_PHASE(4);
     positions<NU, kBlock>(s, s.du, s.dp, nullptr, H);
     __syncthreads();
@@ -1406,7 +1541,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         }
         __syncthreads();
         MPC_PHASE(12);
-        riccati_solve<NU, NX>(s, H, s.du);
+        newton_solve<NU, NX, kBlock>(s, H, s.du);
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
         positions<NU, kBlock>(s, s.u, s.p, s.c, H);
@@ -1589,7 +1724,7 @@ bool all_finite(const double* p, int64_t n) {
 
 template <int NU, int NX, int BLK>
 int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<BLK / 64>::total;
+  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<BLK / 64, NU, NX>::total;
   static bool attr_set = false;  // idempotent; a racing second call sets the same value
   if (!attr_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK>),
