@@ -345,17 +345,30 @@ __device__ __forceinline__ double ratio(double x, double dx) {
   return dx < 0.0 ? -x * __builtin_amdgcn_rcp(dx) : kHuge;
 }
 
-// p[2k+i] = c[2k+i] + sum_{j<=k} Mp[k-j][i][:] . u[j*nu : (j+1)*nu]
+// p[2k+i] = c[2k+i] + sum_{j<=k} Mp[k-j][i][:] . u[j*nu : (j+1)*nu].  The sum over j is split
+// into PARTS interleaved partial sums (threads (t, part)), combined in a fixed order through the
+// per-step scratch s.red — a chain of k/PARTS instead of k dependent steps.  The caller
+// synchronises after (s.red is free at every call site).
 template <int NU, int kBlock>
 __device__ inline void positions(const Lds& s, const double* u, double* out, const double* c, int H) {
-  for (int t = threadIdx.x; t < 2 * H; t += kBlock) {
+  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
+  double* part_sum = s.red;  // [2H][PARTS]
+  for (int e = threadIdx.x; e < 2 * H * PARTS; e += kBlock) {
+    const int t = e / PARTS, part = e - (e / PARTS) * PARTS;
     const int k = t >> 1, i = t & 1;
-    double acc = c ? c[t] : 0.0;
-    for (int j = 0; j <= k; ++j) {
+    double acc = 0.0;
+    for (int j = part; j <= k; j += PARTS) {
       const double* m = s.Mp + ((k - j) * 2 + i) * NU;
 #pragma unroll
       for (int a = 0; a < NU; ++a) acc += m[a] * u[j * NU + a];
     }
+    part_sum[e] = acc;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * H; t += kBlock) {
+    double acc = c ? c[t] : 0.0;
+#pragma unroll
+    for (int part = 0; part < PARTS; ++part) acc += part_sum[t * PARTS + part];
     out[t] = acc;
   }
 }
