@@ -385,6 +385,37 @@ __device__ inline double gp_transpose(const Lds& s, const double* z, int j_a, in
   return acc;
 }
 
+// Gp' z (and, with H0row, H0 u as well) as interleaved partial sums: part_sum[j * PARTS + part]
+// holds the terms k - j = part, part + PARTS, ... (and l = part, part + PARTS, ... of the H0 row),
+// so no thread carries a chain longer than ~H / PARTS; the caller combines the parts in order.
+template <int NU, int kBlock>
+__device__ inline void gpt_parts(const Lds& s, const double* z, const double* H0, const double* u,
+                                 double* part_sum, int n, int H) {
+  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
+  for (int e = threadIdx.x; e < n * PARTS; e += kBlock) {
+    const int j_a = e / PARTS, part = e - (e / PARTS) * PARTS;
+    const int j = j_a / NU, a = j_a - (j_a / NU) * NU;
+    double acc = 0.0;
+    for (int k = j + part; k < H; k += PARTS) {
+      const double* m = s.Mp + (k - j) * 2 * NU;
+      acc += m[a] * z[2 * k] + m[NU + a] * z[2 * k + 1];
+    }
+    if (H0) {
+      const double* h0r = H0 + static_cast<int64_t>(j_a) * n;
+      for (int l = part; l < n; l += PARTS) acc += h0r[l] * u[l];
+    }
+    part_sum[e] = acc;
+  }
+}
+template <int kBlock>
+__device__ __forceinline__ double parts_total(const double* part_sum, int j) {
+  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
+  double acc = part_sum[j * PARTS];
+#pragma unroll
+  for (int part = 1; part < PARTS; ++part) acc += part_sum[j * PARTS + part];
+  return acc;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Newton systems by Riccati recursion.  The condensed Hessian
 //   K = blockdiag(2R + diag(DU_k)) + Gx' blockdiag(2Q + C'S_k C) Gx
@@ -1168,10 +1199,10 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
       }
       __syncthreads();
       // dual residual of the inputs: r_du = H0 u + f + Gp' v + (lUu - lUl)
+      gpt_parts<NU, kBlock>(s, s.v, H0, s.u, s.red, n, H);
+      __syncthreads();
       for (int j = tid; j < n; j += kBlock) {
-        const double* h0r = H0 + static_cast<int64_t>(j) * n;
-        double r = s.f[j] + gp_transpose<NU>(s, s.v, j, H);
-        for (int l = 0; l < n; ++l) r += h0r[l] * s.u[l];
+        double r = s.f[j] + parts_total<kBlock>(s.red, j);
         if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
         s.rdu[j] = r;
         rdm = fmax(rdm, fabs(r));
@@ -1201,7 +1232,9 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     MPC_PHASE(1);
 
     // ---- factor K = H0 + diag(DU) + sum_k Mp' S_k Mp (Riccati), affine rhs ----
-    for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - gp_transpose<NU>(s, s.za, j, H);
+    gpt_parts<NU, kBlock>(s, s.za, nullptr, nullptr, s.red, n, H);
+    __syncthreads();
+    for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - parts_total<kBlock>(s.red, j);
     __syncthreads();
     MPC_PHASE(2);
     if (!riccati_factor<NU, NX>(s, H)) {
@@ -1311,9 +1344,13 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
       const double ratio_g = gap > 0.0 ? gap_aff / gap : 0.0;
       const double sigma_mu = ratio_g * ratio_g * ratio_g * mu;
       s.sc[63] = sigma_mu;  // same value in every thread; kept for P4/P5
+      // Gp' is linear: Gp' za + sigma_mu Gp' zu = Gp' (za + sigma_mu zu), combined in place
+      for (int t = tid; t < 2 * H; t += kBlock) s.zu[t] = s.za[t] + sigma_mu * s.zu[t];
+      __syncthreads();
+      gpt_parts<NU, kBlock>(s, s.zu, nullptr, nullptr, s.red, n, H);
+      __syncthreads();
       for (int j = tid; j < n; j += kBlock)
-        s.du[j] = -s.rdu[j] - (s.rU[j] + sigma_mu * s.rUu[j]) - gp_transpose<NU>(s, s.za, j, H) -
-                  sigma_mu * gp_transpose<NU>(s, s.zu, j, H);
+        s.du[j] = -s.rdu[j] - (s.rU[j] + sigma_mu * s.rUu[j]) - parts_total<kBlock>(s.red, j);
       __syncthreads();
     }
     const double sigma_mu = s.sc[63];
@@ -1543,8 +1580,10 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
           }
         }
         __syncthreads();
+        gpt_parts<NU, kBlock>(s, s.za, nullptr, nullptr, s.red, n, H);
+        __syncthreads();
         for (int j = tid; j < n; j += kBlock) {
-          double r = -s.f[j] - gp_transpose<NU>(s, s.za, j, H);
+          double r = -s.f[j] - parts_total<kBlock>(s.red, j);
           if (a.has_u) {
             const int ai = j % NU;
             if (s.bx[j] != 0.0) r -= s.bx[n + j] - kPolishRho * a.umax[ai];
