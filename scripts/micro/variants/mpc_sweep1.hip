@@ -979,11 +979,12 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
   return t;
 }
 
-// Row sweep of one thread (lane = halfspace step, obstacles o = wave, wave + kWaves, ...).  The
-// rows of kSweep obstacles are loaded together before any is processed.  With two waves per SIMD
-// in both kernel forms the other wave hides the row loads' latency, and a deeper sweep only adds
-// registers: kSweep = 1 (measured against 2: H = 30 QP 0.573 -> 0.542 ms, C5 2.93 -> 2.75 ms,
-// no spills on the 4-state forms).  Inside the body: q (the row), o, r (its workspace index).
+// Row sweep of one thread (lane = halfspace step, obstacles o = wave, wave + 4, ...): the rows
+// of kSweep obstacles are loaded together before any is processed, so kSweep x 8 independent
+// global loads are in flight instead of 8 (the passes are latency-bound at a few hundred rows per
+// thread).  Deeper sweeps cost registers (two workgroups per CU leave 256 per lane) and measured
+// no faster at C5 (kSweep = 4 with one workgroup per CU: 4.06 vs 4.02 ms).  Inside the body: q
+// (the row), o, r (its workspace index).
 constexpr int kSweep = 1;
 #define ROW_SWEEP_BEGIN                                                              \
   for (int o0_ = wave; o0_ < O; o0_ += kSweep * kWaves) {                            \
