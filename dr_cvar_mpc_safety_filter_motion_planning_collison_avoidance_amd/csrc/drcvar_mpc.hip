@@ -508,6 +508,19 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
     }
     const double c0i = s.Cm[i], c1i = s.Cm[kMx + i], c0j = s.Cm[j], c1j = s.Cm[kMx + j];
     const double q2 = 2.0 * s.Qm[i * kMx + j];
+    // loop-invariant operands of stage (b) in registers (the wave fences keep the compiler from
+    // hoisting LDS loads out of the step loop itself)
+    double ai[NX], Bm[NX][NU], R2[NU][NU];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) {
+      ai[m] = s.Am[m * kMx + i];
+#pragma unroll
+      for (int c = 0; c < NU; ++c) Bm[m][c] = s.Bm[m * NU + c];
+    }
+#pragma unroll
+    for (int c = 0; c < NU; ++c)
+#pragma unroll
+      for (int d = 0; d < NU; ++d) R2[c][d] = 2.0 * s.Rm[c * NU + d];
     auto qb = [&](int k) {  // Qb_{k+1} = 2Q + C'S_k C, entry (i, j)
       const double S00 = s.S[k], S01 = s.S[H + k], S11 = s.S[2 * H + k];
       return q2 + c0i * (S00 * c0j + S01 * c1j) + c1i * (S01 * c0j + S11 * c1j);
@@ -539,17 +552,13 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
       }
       wave_lds_fence();
       // (b) every operand in one batch: T columns i and j, U, B, the weights of step k
-      double ti[NX], tj[NX], Um[NX][NU], Bm[NX][NU], du[NU], ai[NX];
+      double ti[NX], tj[NX], Um[NX][NU], du[NU];
 #pragma unroll
       for (int m = 0; m < NX; ++m) {
         ti[m] = s.T[m * kMx + i];
         tj[m] = s.T[m * kMx + j];
-        ai[m] = s.Am[m * kMx + i];
 #pragma unroll
-        for (int c = 0; c < NU; ++c) {
-          Um[m][c] = s.U[m * NU + c];
-          Bm[m][c] = s.Bm[m * NU + c];
-        }
+        for (int c = 0; c < NU; ++c) Um[m][c] = s.U[m * NU + c];
       }
 #pragma unroll
       for (int c = 0; c < NU; ++c) du[c] = s.DU[k * NU + c];
@@ -560,7 +569,7 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
       for (int c = 0; c < NU; ++c)
 #pragma unroll
         for (int d = 0; d < NU; ++d) {
-          double acc = 2.0 * s.Rm[c * NU + d] + (c == d ? du[c] : 0.0);
+          double acc = R2[c][d] + (c == d ? du[c] : 0.0);
 #pragma unroll
           for (int m = 0; m < NX; ++m) acc += Bm[m][c] * Um[m][d];
           Re[c][d] = acc;
