@@ -62,6 +62,7 @@ constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 4;    // active-set corrections
 constexpr double kPolishMerit = 1e-6; // polish only from an iterate this close to the optimum
 constexpr double kPolishDualTol = 1e-7;
+constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
 
 #ifdef DRCVAR_MPC_STAMPS
 // diagnostic build only: per-category shader-clock totals of problem 0..kStampProblems-1
@@ -1607,29 +1608,50 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         positions<NU, kBlock>(s, s.u, s.p, s.c, H);
         __syncthreads();
         MPC_PHASE(13);
-        // multiplier updates nu += rho * (E u - e)
+        // multiplier updates nu += rho * (E u - e); eres = |E u - e|_inf
+        double eres = 0.0;
         if (lane < K) {
           const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
           for (int o = wave; o < O; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
-            if (rows.wA[r] == 2.0) rows.s[r] += kPolishRho * (rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r]);
+            if (rows.wA[r] == 2.0) {
+              const double e = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
+              rows.s[r] += kPolishRho * e;
+              eres = fmax(eres, fabs(e));
+            }
           }
         }
         if (a.has_u) {
           for (int j = tid; j < n; j += kBlock) {
             const int ai = j % NU;
-            if (s.bx[j] != 0.0) s.bx[n + j] += kPolishRho * (s.u[j] - a.umax[ai]);
-            if (s.bx[2 * n + j] != 0.0) s.bx[3 * n + j] += kPolishRho * (a.umin[ai] - s.u[j]);
+            if (s.bx[j] != 0.0) {
+              s.bx[n + j] += kPolishRho * (s.u[j] - a.umax[ai]);
+              eres = fmax(eres, fabs(s.u[j] - a.umax[ai]));
+            }
+            if (s.bx[2 * n + j] != 0.0) {
+              s.bx[3 * n + j] += kPolishRho * (a.umin[ai] - s.u[j]);
+              eres = fmax(eres, fabs(a.umin[ai] - s.u[j]));
+            }
           }
         }
         if (a.has_p) {
           for (int t = tid; t < 2 * H; t += kBlock) {
             const int i = t & 1;
-            if (s.px[t] != 0.0) s.px[2 * H + t] += kPolishRho * (s.p[t] - a.pmax[i]);
-            if (s.px[4 * H + t] != 0.0) s.px[6 * H + t] += kPolishRho * (a.pmin[i] - s.p[t]);
+            if (s.px[t] != 0.0) {
+              s.px[2 * H + t] += kPolishRho * (s.p[t] - a.pmax[i]);
+              eres = fmax(eres, fabs(s.p[t] - a.pmax[i]));
+            }
+            if (s.px[4 * H + t] != 0.0) {
+              s.px[6 * H + t] += kPolishRho * (a.pmin[i] - s.p[t]);
+              eres = fmax(eres, fabs(a.pmin[i] - s.p[t]));
+            }
           }
         }
-        __syncthreads();
+        // The multipliers have converged once the equalities hold to roundoff (a further pass
+        // moves nu by rho * eres and u by ~eres): stop instead of running all kPolishIters.
+        double unused_a = 0.0, unused_b = 0.0;
+        block_sum_max_max<kWaves>(unused_a, eres, unused_b, s.sc);  // uniform; also the barrier
+        if (eres <= kPolishEqTol * scale_d) break;
       }
       // sign conditions; violators move (primal-dual active-set step)
       double bad = 0.0;
