@@ -50,7 +50,7 @@ def test_abi_version_and_strerror():
 
 
 @pytest.mark.parametrize("n,expect", [(1, (64, 2, 128)), (100, (64, 2, 128)), (129, (128, 4, 256)),
-                                      (1000, (256, 4, 512)), (5000, (512, 16, 1024)),
+                                      (1000, (256, 4, 512)), (5000, (256, 20, 1024)), (6000, (512, 16, 1024)),
                                       (10000, (512, 20, 1024)), (16384, (1024, 16, 1024))])
 def test_launch_plan(n, expect):
     b, p, nb = _native.launch_plan(n)

@@ -48,8 +48,8 @@ def test_golden_vectors(golden):
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 63, 64, 65, 100, 128, 129, 300, 512, 513, 1000, 1024,
-                               1025, 2048, 3000, 4096, 4097, 5000, 8192, 8193, 10000, 10240,
-                               10241, 12288, 16384])
+                               1025, 2048, 3000, 4096, 4097, 5000, 5120, 5121, 8192, 8193, 10000,
+                               10240, 10241, 12288, 16384])
 def test_every_launch_plan_random(n):
     rng = np.random.default_rng(n)
     O, T = 2, 3
