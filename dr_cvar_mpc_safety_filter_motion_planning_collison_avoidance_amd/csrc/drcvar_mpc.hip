@@ -1056,6 +1056,9 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     for (int q = 0; q < nx; ++q) acc += ca[q] * x0[q];
     s.c[t] = acc;
   }
+  // f = F1 x0 - F2 xr, summed in this order on purpose: splitting the sum (as the Gp'z sums are)
+  // moved the rounding of f enough to stall one degenerate test problem (generic1, H = 64) at
+  // merit 1e-8 with a failing polish — a fragility to fix at its root, not to paper over here
   for (int j = tid; j < n; j += kBlock) {
     const double* f1 = a.blob + a.off.F1 + static_cast<int64_t>(j) * nx;
     const double* f2 = a.blob + a.off.F2 + static_cast<int64_t>(j) * H * nx;
@@ -1726,17 +1729,27 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   for (int q = tid; q < nx; q += kBlock) s.xs[q] = x0[q];
   __syncthreads();
   positions<NU, kBlock>(s, s.u, s.p, s.c, H);  // positions of the returned inputs (slacks below)
-  const double* A = a.blob + a.off.A;
-  const double* B = a.blob + a.off.B;
-  for (int t = 0; t < H; ++t) {  // x_{t+1} = A x_t + B u_t (core/mpc_filter.py:85-86, :216-217)
-    if (tid < nx) {
+  // x_{t+1} = A x_t + B u_t (core/mpc_filter.py:85-86, :216-217): wave 0, lane q < nx holds x_q,
+  // the state moving between lanes by readlane — no barrier per step
+  if (tid < 64) {
+    const int li = lane < nx ? lane : 0;
+    double Arow[NX], Brow[NU];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) Arow[m] = s.Am[li * kMx + m];  // zero-padded beyond nx
+#pragma unroll
+    for (int c = 0; c < NU; ++c) Brow[c] = s.Bm[li * NU + c];
+    double xv = lane < nx ? x0[lane] : 0.0;
+    for (int t = 0; t < H; ++t) {
       double acc = 0.0;
-      for (int q = 0; q < nx; ++q) acc += A[tid * nx + q] * s.xs[t * nx + q];
-      for (int q = 0; q < NU; ++q) acc += B[tid * NU + q] * s.u[t * NU + q];
-      s.xs[(t + 1) * nx + tid] = acc;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc += Arow[m] * readlane_f64(xv, m);
+#pragma unroll
+      for (int c = 0; c < NU; ++c) acc += Brow[c] * s.u[t * NU + c];
+      xv = lane < nx ? acc : 0.0;
+      if (lane < nx) s.xs[(t + 1) * nx + lane] = acc;
     }
-    __syncthreads();
   }
+  __syncthreads();
   // objective (core/mpc_filter.py:64-76,142-144) and the largest slack
   double obj = 0.0, smax = 0.0;
   if (optimal) {
