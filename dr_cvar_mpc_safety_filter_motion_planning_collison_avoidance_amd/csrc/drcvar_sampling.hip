@@ -4,8 +4,20 @@
 // t >= 1 the N samples are nominal[t] + N(0, noise_cov) (np.random.multivariate_normal), step 0 is
 // the nominal start for every sample (:63).  Here every sample is one Philox4x32-10 call (counter =
 // global sample index and stream, key = seed) -> two 53-bit uniforms -> Box-Muller -> L z, written
-// straight into the [O, T, N, 2] layout the halfspace kernel streams.  Bandwidth-bound on the
-// 16-B store per sample (the fp64 log / sincospi per sample sit under the store time).
+// straight into the [O, T, N, 2] layout the halfspace kernel streams.
+//
+// The per-sample arithmetic is what bounds this kernel, not the 16-B store: with the library's
+// fp64 log (98 VALU instructions) and sincospi (71) plus Philox's 40 quarter-rate 32-bit
+// multiplies it ran at 0.21 of HBM.  So the Box-Muller pieces are written for this input domain:
+//   * Philox rounds use one v_mad_u64_u32 per product (the 64-bit product gives both halves) and
+//     one v_bitop3_b32 (3-input XOR, truth table 0x96) per output word;
+//   * log u1 for u1 in (0, 1): frexp, f = m - 1 with m in [sqrt(1/2), sqrt(2)), s = f / (2 + f),
+//     log(1 + f) = 2 atanh(s) as a degree-21 odd series in s (|s| <= 0.1716: truncation < 1e-17);
+//   * cos/sin of 2 pi u2 straight from the 64 raw bits of u2: the top two bits (rounded) are the
+//     quadrant, the signed remainder |x| <= pi/4 goes through Taylor series to x^15 / x^16;
+//   * sqrt through rsq + Newton (the argument is never denormal);
+// All four agree with the libm functions to a few ulp (tests/test_sampling.py checks the host
+// mirror oracle/philox_sampler.py against numpy's log/sin/cos and the kernel against the mirror).
 
 #include <hip/hip_runtime.h>
 
@@ -16,7 +28,7 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kPerThread = 2;  // samples per thread (independent Philox calls for ILP)
+constexpr int kPerThread = 4;  // samples per thread (independent Philox calls for ILP)
 
 struct Philox {
   uint32_t x[4];
@@ -24,17 +36,18 @@ struct Philox {
 
 __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                 uint32_t k0, uint32_t k1) {
-  constexpr uint32_t kM0 = 0xD2511F53u, kM1 = 0xCD9E8D57u;
+  constexpr uint64_t kM0 = 0xD2511F53u, kM1 = 0xCD9E8D57u;
   constexpr uint32_t kW0 = 0x9E3779B9u, kW1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(kM0, c0), lo0 = kM0 * c0;
-    const uint32_t hi1 = __umulhi(kM1, c2), lo1 = kM1 * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    const uint64_t p0 = kM0 * c0, p1 = kM1 * c2;  // one v_mad_u64_u32 each
+    uint32_t n0, n2;  // hi(p1) ^ c1 ^ k0, hi(p0) ^ c3 ^ k1 (the key words are uniform: SGPRs)
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(static_cast<uint32_t>(p1 >> 32)), "v"(c1), "s"(k0));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(static_cast<uint32_t>(p0 >> 32)), "v"(c3), "s"(k1));
     c0 = n0;
-    c1 = lo1;
+    c1 = static_cast<uint32_t>(p1);
     c2 = n2;
-    c3 = lo0;
+    c3 = static_cast<uint32_t>(p0);
     k0 += kW0;
     k1 += kW1;
   }
@@ -45,6 +58,82 @@ __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32
 __device__ __forceinline__ double uniform53(uint32_t hi, uint32_t lo) {
   const uint64_t v = (static_cast<uint64_t>(hi) << 32 | lo) >> 11;
   return (static_cast<double>(v) + 0.5) * 0x1.0p-53;
+}
+
+// log(x) for 0 < x <= 1 (normal).  x = m 2^e with m in [sqrt(1/2), sqrt(2)); f = m - 1 is exact;
+// log m = 2 atanh(s), s = f / (2 + f), summed as 2 s + s^3 P(s^2) with P the atanh series to s^21.
+__device__ __forceinline__ double log_unit(double x) {
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  int e = __builtin_amdgcn_frexp_exp(x);
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  e = lo ? e - 1 : e;
+  const double f = m - 1.0;
+  const double d = 2.0 + f;  // in [1.7, 2.5]: a plain reciprocal + Newton division is exact enough
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(fma(-d, r, 1.0), r, r);
+  r = fma(fma(-d, r, 1.0), r, r);
+  double sq = f * r;
+  sq = fma(fma(-d, sq, f), r, sq);
+  const double z = sq * sq;
+  double p = 2.0 / 21.0;
+  p = fma(p, z, 2.0 / 19.0);
+  p = fma(p, z, 2.0 / 17.0);
+  p = fma(p, z, 2.0 / 15.0);
+  p = fma(p, z, 2.0 / 13.0);
+  p = fma(p, z, 2.0 / 11.0);
+  p = fma(p, z, 2.0 / 9.0);
+  p = fma(p, z, 2.0 / 7.0);
+  p = fma(p, z, 2.0 / 5.0);
+  p = fma(p, z, 2.0 / 3.0);
+  const double logm = fma(sq * z, p, sq + sq);
+  constexpr double kLn2Hi = 0x1.62e42fefa3800p-1, kLn2Lo = 0x1.ef35793c76730p-45;
+  const double de = static_cast<double>(e);
+  return fma(de, kLn2Hi, fma(de, kLn2Lo, logm));
+}
+
+// sqrt(-2 log u1).  The argument is >= 2^-53 (u1 <= 1 - 2^-54), never denormal, so rsq + two
+// Newton-Raphson steps (Goldschmidt form) replace the library sqrt and its rescaling.
+__device__ __forceinline__ double box_muller_radius(double u1) {
+  const double y = -2.0 * log_unit(u1);
+  double h = 0.5 * __builtin_amdgcn_rsq(y), r = y * (h + h);
+  const double e = fma(-r, h, 0.5);
+  r = fma(r, e, r);
+  h = fma(h, e, h);
+  return fma(fma(-r, r, y), h, r);
+}
+
+// (cos, sin)(2 pi w / 2^64): quadrant q = round(w / 2^62) mod 4, remainder x = 2 pi (w - q 2^62) /
+// 2^64 in [-pi/4, pi/4) (53 significant bits of it kept), Taylor series to x^15 (sin) / x^16 (cos).
+__device__ __forceinline__ void cos_sin_turn(uint32_t whi, uint32_t wlo, double* cs, double* sn) {
+  const uint64_t w = static_cast<uint64_t>(whi) << 32 | wlo;
+  const uint32_t q = static_cast<uint32_t>((w + (uint64_t{1} << 61)) >> 62);
+  const int64_t rem = static_cast<int64_t>(w - (static_cast<uint64_t>(q) << 62)) >> 11;
+  constexpr double kTurn = 6.28318530717958647692 * 0x1.0p-53;
+  const double x = static_cast<double>(rem) * kTurn;
+  const double z = x * x;
+  double ps = -1.0 / 1307674368000.0;
+  ps = fma(ps, z, 1.0 / 6227020800.0);
+  ps = fma(ps, z, -1.0 / 39916800.0);
+  ps = fma(ps, z, 1.0 / 362880.0);
+  ps = fma(ps, z, -1.0 / 5040.0);
+  ps = fma(ps, z, 1.0 / 120.0);
+  ps = fma(ps, z, -1.0 / 6.0);
+  const double s = fma(x * z, ps, x);
+  double pc = 1.0 / 20922789888000.0;
+  pc = fma(pc, z, -1.0 / 87178291200.0);
+  pc = fma(pc, z, 1.0 / 479001600.0);
+  pc = fma(pc, z, -1.0 / 3628800.0);
+  pc = fma(pc, z, 1.0 / 40320.0);
+  pc = fma(pc, z, -1.0 / 720.0);
+  pc = fma(pc, z, 1.0 / 24.0);
+  pc = fma(pc, z, -0.5);
+  const double c = fma(z, pc, 1.0);
+  // theta = q pi/2 + x: q=0 (c, s), 1 (-s, c), 2 (-c, -s), 3 (s, -c)
+  const bool swap = q & 1;
+  const double a = swap ? s : c, b = swap ? c : s;
+  *cs = ((q + 1) & 2) ? -a : a;
+  *sn = (q & 2) ? -b : b;
 }
 
 struct SampleArgs {
@@ -75,11 +164,9 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
         const uint64_t g = static_cast<uint64_t>(u) * static_cast<uint64_t>(a.N) + static_cast<uint64_t>(i);
         const Philox r = philox4x32_10(static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
                                        a.s0, a.s1, a.k0, a.k1);
-        const double u1 = uniform53(r.x[0], r.x[1]);
-        const double u2 = uniform53(r.x[2], r.x[3]);
-        const double rad = sqrt(-2.0 * log(u1));
+        const double rad = box_muller_radius(uniform53(r.x[0], r.x[1]));
         double sn, cs;
-        sincospi(2.0 * u2, &sn, &cs);
+        cos_sin_turn(r.x[2], r.x[3], &cs, &sn);
         const double z0 = rad * cs, z1 = rad * sn;
         x = nx + a.l00 * z0;
         y = ny + (a.l10 * z0 + a.l11 * z1);

@@ -1,0 +1,28 @@
+"""Times drcvar_sample_trajectories_f64 refilling a resident C5-shaped batch (256 x 50 x 10000
+samples, 2.05 GB) and prints the write bandwidth; with DRCVAR_DIAG_LIB it times a variant build."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.simulation import obstacles
+
+O, T, N = 256, 50, 10000
+dev = torch.device("cuda", 0)
+out = torch.empty((O, T, N, 2), dtype=torch.float64, device=dev)
+nominal = torch.zeros((O, T, 2), dtype=torch.float64, device=dev)
+launch = lambda: obstacles.sample_trajectories_device(nominal, N, seed=11, out=out)
+for _ in range(3):
+    launch()
+torch.cuda.synchronize()
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+for _ in range(20):
+    launch()
+b.record()
+torch.cuda.synchronize()
+sec = a.elapsed_time(b) * 1e-3 / 20
+print(f"sampler {O}x{T}x{N}: {sec * 1e3:.3f} ms, {O * T * N * 16 / sec / 1e12:.2f} TB/s written, "
+      f"checksum {out[:, 1:].sum().item():.6e} sd {out[:, 1:].std().item():.6f}")

@@ -2,9 +2,12 @@
 
 CPU: the host mirror reproduces the reference's RNG stream bit for bit (the golden vectors were
 drawn by the reference's own generate_obstacle_scenarios with seed 42) and the layout packer is
-a pure transpose.  GPU: the Philox sampler's distribution (moments, correlation, normality),
-determinism and stream separation, the noise-free first step, strided outputs, and the
-sampler -> halfspace kernel pipeline against the C oracle on the same samples.
+a pure transpose; the device generator's NumPy mirror (oracle/philox_sampler.py) reproduces the
+published Philox4x32-10 known-answer vectors and its log / cos / sin series agree with extended-
+precision references.  GPU: the kernel against that mirror value for value, the sampler's
+distribution (moments, correlation, normality), determinism and stream separation, the noise-free
+first step, strided outputs, and the sampler -> halfspace kernel pipeline against the C oracle on
+the same samples.
 """
 import os
 
@@ -47,6 +50,41 @@ def test_pack_layout_is_a_transpose():
     np.testing.assert_array_equal(packed.numpy(), np.stack([np.transpose(t[:, :9], (1, 0, 2)) for t in trs]))
 
 
+# Random123 kat_vectors, philox4x32 10 rounds: (counter, key) -> output
+PHILOX_KAT = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+              ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+              ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+               (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+
+
+@pytest.mark.parametrize("ctr,key,want", PHILOX_KAT)
+def test_philox_mirror_known_answers(ctr, key, want):
+    from oracle import philox_sampler as ps
+    got = ps.philox4x32_10(*ctr, *key)
+    assert tuple(int(x) for x in got) == want
+
+
+def test_sampler_series_accuracy():
+    """The kernel's log / cos / sin series (restated by the mirror) against long-double references:
+    log within 2 ulp over (0, 1), cos / sin of 2 pi w / 2^64 within 4e-16."""
+    from oracle import philox_sampler as ps
+    rng = np.random.default_rng(3)
+    v = rng.integers(0, 2 ** 53, size=400_000, dtype=np.uint64)
+    u = np.concatenate([(v.astype(np.float64) + 0.5) * 2.0 ** -53,
+                        [2.0 ** -54, 1 - 2.0 ** -53, 0.5, 0.25, 0.7071067811865475, 0.7071067811865476]])
+    ref = np.log(u.astype(np.longdouble))
+    ulp = np.spacing(np.abs(ref.astype(np.float64)))
+    assert np.max(np.abs(ps.log_unit(u) - ref) / ulp) <= 2.0
+    w = np.concatenate([rng.integers(0, 2 ** 64 - 1, size=400_000, dtype=np.uint64, endpoint=True),
+                        np.array([0, 1 << 61, (1 << 61) - 1, 1 << 62, 3 << 62, 2 ** 64 - 1], dtype=np.uint64)])
+    c, s = ps.cos_sin_turn(w >> np.uint64(32), w & np.uint64(0xFFFFFFFF))
+    w53 = w & ~np.uint64(0x7FF)                   # the series sees the angle to 53 bits (rem >> 11)
+    pi = np.longdouble("3.14159265358979323846264338327950288")
+    th = (w53.astype(np.longdouble) / np.longdouble(2.0 ** 64)) * (2 * pi)
+    assert np.max(np.abs(c - np.cos(th))) < 4e-16 and np.max(np.abs(s - np.sin(th))) < 4e-16
+    assert np.allclose(c * c + s * s, 1.0, atol=5e-16, rtol=0)
+
+
 @pytest.fixture(scope="module")
 def dev():
     import torch
@@ -82,6 +120,26 @@ def test_device_sampler_moments_and_normality(dev):
                 z = np.linalg.solve(L, d.T)
                 for comp in z:
                     assert stats.kstest(comp, "norm").pvalue > 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("O,T,N,seed,stream,zero_first", [(2, 3, 5000, 123, 0, True),
+                                                          (3, 5, 777, 2 ** 40 + 9, 2 ** 33 + 1, False),
+                                                          (1, 2, 1, 0, 0, True)])
+def test_device_sampler_matches_mirror(dev, O, T, N, seed, stream, zero_first):
+    """Kernel vs oracle/philox_sampler.py on the same (seed, stream, indices): equal up to the
+    FMA contraction of the series (a few ulp)."""
+    import torch
+    from oracle import philox_sampler as ps
+    cov = np.array([[0.04, 0.012], [0.012, 0.02]])
+    nom = _nominal(dev, O, T)
+    got = ob.sample_trajectories_device(nom, N, cov, seed=seed, stream_offset=stream,
+                                        zero_first_step=zero_first).cpu().numpy()
+    L = np.linalg.cholesky(cov)
+    want = ps.sample_trajectories(nom.cpu().numpy(), N, (L[0, 0], L[1, 0], L[1, 1]), seed, stream,
+                                  zero_first)
+    assert got.shape == want.shape
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-14)
 
 
 @pytest.mark.gpu
