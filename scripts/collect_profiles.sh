@@ -11,6 +11,8 @@ O=gpurun_out
 [ -f $O/bench_c5.log ] && grep '^{' $O/bench_c5.log | tail -1 > $D/bench_c5.json
 [ -f $O/prof/run_kernel_stats.csv ] && cp $O/prof/run_kernel_stats.csv $D/bench_c3_graph_kernel_stats.csv
 [ -f $O/prof/run_domain_stats.csv ] && cp $O/prof/run_domain_stats.csv $D/bench_c3_graph_domain_stats.csv
+[ -f $O/mpc_bench.log ] && grep -v amdgpu.ids $O/mpc_bench.log > $D/mpc_bench.log
+[ -f $O/mpcprof/run_kernel_stats.csv ] && cp $O/mpcprof/run_kernel_stats.csv $D/mpc_bench_kernel_stats.csv
 for w in c3 c5; do
   for k in fetch write; do
     f=$(find $O/pmc_${k}_$w -name '*counter_collection.csv' 2>/dev/null | head -1)

@@ -15,7 +15,7 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-for s in ${STEPS:-pytest smoke bench bench_c5 prof pmc}; do
+for s in ${STEPS:-pytest smoke bench bench_c5 prof mpcprof pmc}; do
   case $s in
     pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -23,6 +23,7 @@ for s in ${STEPS:-pytest smoke bench bench_c5 prof pmc}; do
     bench_eager) step bench_eager 600 python bench.py --launch eager --no-large --no-cpu-baseline ;;
     bench_c5) step bench_c5 600 python bench.py --workload c5 --steps 200 --warmup 10 --graph-batch 10 --no-large --no-cpu-baseline ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 2000 --no-cpu-baseline ;;
+    mpcprof) step mpc_bench 300 rocprofv3 --kernel-trace --stats -d $OUT/mpcprof -o run --output-format csv -- python3 scripts/mpc_bench.py ;;
     pmc)
       for w in c3 c5; do
         step pmc_fetch_$w 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$w -o run --output-format csv -- python3 bench.py --workload $w --steps 20 --warmup 2 --graph-batch 10 --no-large --no-cpu-baseline
