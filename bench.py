@@ -90,10 +90,38 @@ def cpu_baseline(samples, ego, params, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return ref, {"value": reps * units / el, "unit": "halfspace-constraints/s", "cores": 1,
-                 "kind": "port",
-                 "sample": f"{reps} full batches x {units} units of the same workload "
-                           f"({el:.1f} s, oracle/drcvar_oracle.c quickselect, 1 thread)"}
+    base = {"value": reps * units / el, "unit": "halfspace-constraints/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} full batches x {units} units of the same workload "
+                      f"({el:.1f} s, oracle/drcvar_oracle.c quickselect, 1 thread)"}
+    # the same port on every core of this process's CPU share (the GPU box shows
+    # the whole machine in os.cpu_count(); one GPU's share is 16 threads)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        c_oracle.safe_halfspaces(s, e, *args, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s / 3:
+            break
+    base["all_cores"] = {"value": reps * units / el, "cores": threads,
+                         "sample": f"{reps} full batches ({el:.1f} s), units split over {threads} threads"}
+    # §8d(ii): the reference's algorithm class -- the two LPs per unit (core/risk_metrics.py
+    # :87-125, :182-213) through scipy's HiGHS (oracle/lp_highs.py), one core, a few units
+    from oracle import lp_highs
+    flat_s, flat_h = s.reshape(units, s.shape[2], 2), ref.reshape(units, -1)[:, 3:5]
+    done, t0 = 0, time.perf_counter()
+    while done < units:
+        lp_highs.solve_cvar_lp(flat_s[done], flat_h[done], params.alpha, params.delta,
+                               params.robot_radius, params.obstacle_radius)
+        lp_highs.solve_dr_cvar_lp(flat_s[done], flat_h[done], params.alpha, params.delta,
+                                  params.epsilon, params.robot_radius, params.obstacle_radius)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s / 3:
+            break
+    base["lp_highs"] = {"value": done / el, "cores": 1,
+                        "sample": f"{done} units x 2 LPs ({el:.1f} s, scipy HiGHS, oracle/lp_highs.py)"}
+    return ref, base
 
 
 class Stepper:
