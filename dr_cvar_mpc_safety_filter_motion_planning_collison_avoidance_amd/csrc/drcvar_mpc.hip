@@ -1260,46 +1260,25 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     __syncthreads();
     MPC_PHASE(14);
 
-    // ---- P2: affine step length ----
+    // ---- P2+P3: affine step length, affine gap, corrector rhs — one sweep of the rows ----
+    // The corrector rhs sums do not depend on the affine step a_aff, and a row's affine gap
+    // (w + a dw)(l + a dl) is a quadratic in it: the sweep keeps sum w l, sum (w dl + l dw) and
+    // sum dw dl per thread and evaluates the quadratic once a_aff is known (the rows used to be
+    // swept twice, before and after the block minimum).
     double amax = kHuge;
-    if (lane < K) {
-      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-      const double d0 = s.dpa[2 * lane], d1 = s.dpa[2 * lane + 1];
-      ROW_SWEEP_BEGIN
-        const HsLin l = hs_lin(q, p0, p1);
-        amax = fmin(amax, hs_ratio(q, hs_affine(q, l, q.h0 * d0 + q.h1 * d1)));
-      ROW_SWEEP_END
-    }
-    if (a.has_u) {
-      for (int j = tid; j < n; j += kBlock) {
-        const int ai = j % NU;
-        const PairState q = box_state(s, n, j);
-        const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
-        amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dua[j], 0.0, false)));
-      }
-    }
-    if (a.has_p) {
-      for (int t = tid; t < 2 * H; t += kBlock) {
-        const int i = t & 1;
-        const PairState q = pos_state(s, H, t);
-        const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
-        amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dpa[t], 0.0, false)));
-      }
-    }
-    const double a_aff = fmin(1.0, block_min<kWaves>(amax, s.sc));
-
-    // ---- P3: affine gap and the corrector rhs as base + sigma*mu * unit ----
     {
       double acc[4] = {0, 0, 0, 0};
-      double gap_aff = 0.0;
+      double gq0 = 0.0, gq1 = 0.0, gq2 = 0.0;
       if (lane < K) {
         const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
         const double d0 = s.dpa[2 * lane], d1 = s.dpa[2 * lane + 1];
         ROW_SWEEP_BEGIN
           const HsLin l = hs_lin(q, p0, p1);
           const RowDir d = hs_affine(q, l, q.h0 * d0 + q.h1 * d1);
-          gap_aff += (q.wA + a_aff * d.dwA) * (q.lA + a_aff * d.dlA) +
-                     (q.wB + a_aff * d.dwB) * (q.lB + a_aff * d.dlB);
+          amax = fmin(amax, hs_ratio(q, d));
+          gq0 += q.wA * q.lA + q.wB * q.lB;
+          gq1 += (q.wA * d.dlA + q.lA * d.dwA) + (q.wB * d.dlB + q.lB * d.dwB);
+          gq2 += d.dwA * d.dlA + d.dwB * d.dlB;
           const double rhoA_b = l.DA * l.rpA - q.lA - d.dwA * d.dlA * l.iwA;
           const double rhoB_b = l.DB * l.rpB - q.lB - d.dwB * d.dlB * l.iwB;
           const double cb = rhoA_b - l.DA * (-l.rds + rhoA_b + rhoB_b) * l.isig;
@@ -1310,9 +1289,28 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
           acc[3] += cu * q.h1;
         ROW_SWEEP_END
       }
+      // published by the barriers of block_min below (positions' reads of s.red ended at the
+      // barrier before this sweep)
 #pragma unroll
       for (int q = 0; q < 4; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
-      __syncthreads();
+      if (a.has_u) {
+        for (int j = tid; j < n; j += kBlock) {
+          const int ai = j % NU;
+          const PairState q = box_state(s, n, j);
+          const PairLin l = pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]);
+          amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dua[j], 0.0, false)));
+        }
+      }
+      if (a.has_p) {
+        for (int t = tid; t < 2 * H; t += kBlock) {
+          const int i = t & 1;
+          const PairState q = pos_state(s, H, t);
+          const PairLin l = pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]);
+          amax = fmin(amax, pair_ratio(q, pair_dir(q, l, 0.0, s.dpa[t], 0.0, false)));
+        }
+      }
+      const double a_aff = fmin(1.0, block_min<kWaves>(amax, s.sc));
+      double gap_aff = fma(fma(gq2, a_aff, gq1), a_aff, gq0);
       if (wave == 0 && lane < H) {
         double tot[4];
 #pragma unroll
