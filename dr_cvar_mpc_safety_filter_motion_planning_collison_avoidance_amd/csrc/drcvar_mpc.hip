@@ -48,6 +48,7 @@ namespace {
 // BLK parameter; helpers take the wave count as a template argument.
 constexpr int kMaxWaves = 8;
 constexpr int kFewProblems = 128;  // at most this many problems per launch: 512-thread form
+constexpr int kShortHorizon = 32;  // horizon capacity of the 128-thread (many problems) form
 constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
 constexpr int kRowArrays = 8; // h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
 constexpr int kBestPad = 128; // best iterate u (n <= DRCVAR_MPC_MAX_DECISION)
@@ -60,7 +61,7 @@ constexpr int kPerStepQ = 7;          // per-step partial sums carried by one re
 constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
 constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 4;    // active-set corrections
-constexpr double kPolishMerit = 1e-6; // polish only from an iterate this close to the optimum
+constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
 constexpr double kPolishDualTol = 1e-7;
 constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
 
@@ -175,10 +176,10 @@ constexpr int kMx = DRCVAR_MPC_MAX_STATES;  // row stride of the state-dimension
 constexpr int kMu = DRCVAR_MPC_MAX_INPUTS;
 // NW waves per workgroup (the per-step partial sums), NU inputs and NX (padded) states (the
 // per-step Riccati factors and, for NX <= 4, the parallel-scan buffers)
-template <int NW, int NU, int NX>
+template <int NW, int NU, int NX, int HMX = DRCVAR_MPC_MAX_HORIZON>
 struct LdsPlan {
-  static constexpr int NMAX = DRCVAR_MPC_MAX_DECISION;
-  static constexpr int HM = DRCVAR_MPC_MAX_HORIZON;
+  static constexpr int HM = HMX;  // horizon capacity of the plan
+  static constexpr int NMAX = NU * HM < DRCVAR_MPC_MAX_DECISION ? NU * HM : DRCVAR_MPC_MAX_DECISION;
   static constexpr int Am = 0;
   static constexpr int Bm = Am + kMx * kMx;
   static constexpr int Cm = Bm + kMx * kMu;
@@ -218,10 +219,15 @@ struct LdsPlan {
 static_assert(LdsPlan<4, 4, 4>::total * 8 <= 80 * 1024, "256-thread plan: two workgroups per CU");
 static_assert(LdsPlan<4, 4, 8>::total * 8 <= 80 * 1024, "256-thread plan: two workgroups per CU");
 static_assert(LdsPlan<8, 4, 8>::total * 8 <= 160 * 1024, "512-thread plan exceeds the LDS");
+static_assert(LdsPlan<2, 2, 4, kShortHorizon>::total * 8 <= 40 * 1024,
+              "128-thread short-horizon plan, two inputs: four workgroups per CU");
+static_assert(LdsPlan<2, 4, 4, kShortHorizon>::total * 8 <= 160 * 1024 / 3 &&
+                  LdsPlan<2, 4, 8, kShortHorizon>::total * 8 <= 160 * 1024 / 3,
+              "128-thread short-horizon plan: at least three workgroups per CU");
 
-template <int NW, int NU, int NX>
+template <int NW, int NU, int NX, int HMX>
 __device__ inline Lds carve(double* base) {
-  using P = LdsPlan<NW, NU, NX>;
+  using P = LdsPlan<NW, NU, NX, HMX>;
   Lds s;
   s.Am = base + P::Am;
   s.Bm = base + P::Bm;
@@ -430,6 +436,16 @@ __device__ __forceinline__ double parts_total(const double* part_sum, int j) {
 // O(H nx^3) per factorisation and O(H nx^2) per solve instead of O(n^3) / O(n^2), and no n x n
 // matrix in LDS.  P is formed from its lower triangle and mirrored, so it is exactly symmetric (an
 // unsymmetrised recursion drifts: ~1e-4 relative error at H = 50 in the prototype, 1e-12 with).
+// Near an interior-point solution Re_k carries barrier weights up to ~1e11 and its computed
+// inverse is only cond(Re) * eps accurate; in the form above that error goes straight into P
+// (-L'dKg), and on rare problems P loses definiteness (diagonal -2e3 where ~1e1 was right) until a
+// pivot fails.  A factorisation that fails is therefore repeated in the gain-stationary form
+//   P_k = Qb_k + A'P A - L'Kg - Kg'L + Kg'Re Kg      (= the form above when Kg = Re^-1 L exactly)
+// whose error in Kg enters only to second order, as dKg' Re dKg >= 0 (the Joseph form's property
+// without its extra hand-off).  It is not the default: measured on every test problem it costs
+// interior-point iterations (H = 20: 9 -> 15), its P no longer matching the gains the solves use.
+// Close to the optimum (merit <= kPolishMerit) a failed pivot is the normal end of the interior-
+// point phase and the polish takes over instead.
 // One wave runs the recursion (lanes = matrix entries); its LDS hand-offs need no barrier.
 // ---------------------------------------------------------------------------------------------
 // LDS instructions of one wave complete in issue order; this only keeps the compiler from moving
@@ -489,7 +505,7 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[N
 // model matrices are zero-padded in LDS (setup), so every padded entry of P, T, U, Kg is exactly
 // zero and the loops carry no runtime bounds — every LDS operand of a stage is loaded in one batch.
 // Two wave-local LDS hand-offs per step.  Returns false (uniformly) on a non-positive pivot.
-template <int NU, int NX>
+template <int NU, int NX, bool kStationary = false>
 __device__ inline bool riccati_factor(const Lds& s, int H) {
   const int tid = threadIdx.x, lane = tid & 63;
   double* flag = s.sc + 62;
@@ -576,7 +592,7 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
           Re[c][d] = acc;
         }
       ok = spd_inverse<NU>(Re, Ri);
-      double Li[NU], Lj[NU], Kj[NU];
+      double Li[NU], Lj[NU], Ki[NU], Kj[NU];
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
         double li = 0.0, lj = 0.0;
@@ -590,21 +606,44 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
       }
 #pragma unroll
       for (int c = 0; c < NU; ++c) {
-        double acc = 0.0;
+        double acc = 0.0, acci = 0.0;
 #pragma unroll
-        for (int d = 0; d < NU; ++d) acc += Ri[c][d] * Lj[d];
+        for (int d = 0; d < NU; ++d) {
+          acc += Ri[c][d] * Lj[d];
+          acci += Ri[c][d] * Li[d];
+        }
         Kj[c] = acc;
+        Ki[c] = acci;  // only the stationary form reads it
       }
       if (lane < NX2 && i == j) {
 #pragma unroll
         for (int c = 0; c < NU; ++c) s.Kg[(k * NU + c) * NX + j] = Kj[c];
       }
       if (lane < NX2 && k > 0 && i >= j) {
+        // Qb + A'P A - L'Kg - Kg'L + Kg'Re Kg, entry (i, j); Re_cd = Rb + B'U recomputed from the
+        // registers it was formed from (the inversion overwrote it)
         double acc = qnext;
 #pragma unroll
         for (int m = 0; m < NX; ++m) acc += ai[m] * tj[m];
+        if constexpr (kStationary) {
+          double corr = 0.0;
 #pragma unroll
-        for (int c = 0; c < NU; ++c) acc -= Li[c] * Kj[c];
+          for (int c = 0; c < NU; ++c) {
+            double rk = 0.0;
+#pragma unroll
+            for (int d = 0; d < NU; ++d) {
+              double re = R2[c][d] + (c == d ? du[c] : 0.0);
+#pragma unroll
+              for (int m = 0; m < NX; ++m) re += Bm[m][c] * Um[m][d];
+              rk += re * Kj[d];
+            }
+            corr += Ki[c] * rk - Li[c] * Kj[c] - Ki[c] * Lj[c];
+          }
+          acc += corr;
+        } else {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) acc -= Li[c] * Kj[c];
+        }
         s.P[i * kMx + j] = acc;
         s.P[j * kMx + i] = acc;
       }
@@ -796,9 +835,9 @@ __device__ inline void scan_maps(double* M, double* V, int H, int dir) {
   }
 }
 
-template <int NU, int NX, int kBlock>
+template <int NU, int NX, int kBlock, int HMX>
 __device__ inline void riccati_solve_scan(const Lds& s, int H, double* x) {
-  static_assert(NX <= 4 && DRCVAR_MPC_MAX_HORIZON * 4 <= kBlock, "one thread per map row");
+  static_assert(NX <= 4 && HMX * 4 <= kBlock, "one thread per map row");
   const int t = threadIdx.x, k = t / NX, i = t - (t / NX) * NX;
   const bool own = t < H * NX;
   double* M = s.SM;
@@ -865,10 +904,10 @@ __device__ inline void riccati_solve_scan(const Lds& s, int H, double* x) {
 }
 
 // K x = b: the parallel scan for NX <= 4, the wave-serial recursion otherwise
-template <int NU, int NX, int kBlock>
+template <int NU, int NX, int kBlock, int HMX>
 __device__ inline void newton_solve(const Lds& s, int H, double* x) {
   if constexpr (NX <= 4) {
-    riccati_solve_scan<NU, NX, kBlock>(s, H, x);
+    riccati_solve_scan<NU, NX, kBlock, HMX>(s, H, x);
   } else {
     riccati_solve<NU, NX>(s, H, x);
   }
@@ -1012,7 +1051,10 @@ constexpr int kSweep = 1;
   }                   \
   }
 
-template <int NU, int NX, int BLK>
+// BLK threads per problem; HMX the horizon capacity of its LDS plan.  Every form targets two
+// waves per SIMD (HIP's second launch bound; VGPR budget 256): 512 and 256 threads with two
+// workgroups per CU, 128 threads with four.
+template <int NU, int NX, int BLK, int HMX>
 __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   constexpr int kBlock = BLK;
   constexpr int kWaves = BLK / 64;
@@ -1021,7 +1063,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
-  const Lds s = carve<kWaves, NU, NX>(lds_raw);
+  const Lds s = carve<kWaves, NU, NX, HMX>(lds_raw);
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + b * a.ws_pp;
 #ifdef DRCVAR_MPC_STAMPS
@@ -1058,7 +1100,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   }
   // f = F1 x0 - F2 xr, summed in this order on purpose: splitting the sum (as the Gp'z sums are)
   // moved the rounding of f enough to stall one degenerate test problem (generic1, H = 64) at
-  // merit 1e-8 with a failing polish — a fragility to fix at its root, not to paper over here
+  // merit 1e-8 with a failing polish (degenerate active sets defeat the polish)
   for (int j = tid; j < n; j += kBlock) {
     const double* f1 = a.blob + a.off.F1 + static_cast<int64_t>(j) * nx;
     const double* f2 = a.blob + a.off.F2 + static_cast<int64_t>(j) * H * nx;
@@ -1238,7 +1280,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         best_it = it;
         for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];
       }
-      if (best_merit < 1e-6 && it - best_it >= 8) break;  // stalled at the accuracy floor
+      if (best_merit < kPolishMerit && it - best_it >= 8) break;  // stalled at the accuracy floor
     }
     const double gap = mu * m_ineq;
     MPC_PHASE(1);
@@ -1249,12 +1291,15 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - parts_total<kBlock>(s.red, j);
     __syncthreads();
     MPC_PHASE(2);
-    if (!riccati_factor<NU, NX>(s, H)) {
+    // A failed pivot close to the optimum hands over to the polish (the usual end of a solve
+    // whose barrier weights have outgrown fp64); further out the stationary form takes over.
+    if (!riccati_factor<NU, NX>(s, H) &&
+        (best_merit <= kPolishMerit || !riccati_factor<NU, NX, true>(s, H))) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
     MPC_PHASE(3);
-    newton_solve<NU, NX, kBlock>(s, H, s.dua);
+    newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua);
     MPC_PHASE(4);
     positions<NU, kBlock>(s, s.dua, s.dpa, nullptr, H);
     __syncthreads();
@@ -1365,7 +1410,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     }
     const double sigma_mu = s.sc[63];
     MPC_PHASE(5);
-    newton_solve<NU, NX, kBlock>(s, H, s.du);
+    newton_solve<NU, NX, kBlock, HMX>(s, H, s.du);
     MPC_PHASE(4);
     positions<NU, kBlock>(s, s.du, s.dp, nullptr, H);
     __syncthreads();
@@ -1556,7 +1601,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         __syncthreads();
       }
       MPC_PHASE(10);
-      if (!riccati_factor<NU, NX>(s, H)) break;
+      if (!riccati_factor<NU, NX>(s, H) && !riccati_factor<NU, NX, true>(s, H)) break;
       MPC_PHASE(11);
       for (int pass = 0; pass < kPolishIters; ++pass) {
         // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
@@ -1603,7 +1648,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         }
         __syncthreads();
         MPC_PHASE(12);
-        newton_solve<NU, NX, kBlock>(s, H, s.du);
+        newton_solve<NU, NX, kBlock, HMX>(s, H, s.du);
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
         positions<NU, kBlock>(s, s.u, s.p, s.c, H);
@@ -1815,18 +1860,18 @@ bool all_finite(const double* p, int64_t n) {
   return true;
 }
 
-template <int NU, int NX, int BLK>
+template <int NU, int NX, int BLK, int HMX = DRCVAR_MPC_MAX_HORIZON>
 int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<BLK / 64, NU, NX>::total;
+  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<BLK / 64, NU, NX, HMX>::total;
   static bool attr_set = false;  // idempotent; a racing second call sets the same value
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK, HMX>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK>), dim3(static_cast<unsigned>(n_problems)),
+  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK, HMX>), dim3(static_cast<unsigned>(n_problems)),
                      dim3(BLK), lds_bytes, stream, args);
   return DRCVAR_OK;
 }
@@ -1834,13 +1879,19 @@ int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
 template <int NU>
 int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
   // state dimension padded to 4 or 8 (the Riccati sweeps are unrolled over it); a launch of a
-  // few problems cannot fill the chip, so each problem gets 512 threads
+  // few problems cannot fill the chip, so each problem gets 512 threads.  Many problems with a
+  // short horizon take the 128-thread form: its LDS plan (horizon <= kShortHorizon) fits four
+  // workgroups per CU (three with four inputs), twice the problems in flight of the 256-thread
+  // form.
   const bool few = n_problems <= kFewProblems;
+  const bool short_h = args.H <= kShortHorizon;
   if (args.nx <= 4)
     return few ? launch<NU, 4, 512>(args, n_problems, stream)
-               : launch<NU, 4, 256>(args, n_problems, stream);
+               : short_h ? launch<NU, 4, 128, kShortHorizon>(args, n_problems, stream)
+                         : launch<NU, 4, 256>(args, n_problems, stream);
   return few ? launch<NU, 8, 512>(args, n_problems, stream)
-             : launch<NU, 8, 256>(args, n_problems, stream);
+             : short_h ? launch<NU, 8, 128, kShortHorizon>(args, n_problems, stream)
+                       : launch<NU, 8, 256>(args, n_problems, stream);
 }
 
 }  // namespace
