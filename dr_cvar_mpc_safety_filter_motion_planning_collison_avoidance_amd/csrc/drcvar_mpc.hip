@@ -60,7 +60,7 @@ constexpr double kHuge = 1e300;
 constexpr int kPerStepQ = 7;          // per-step partial sums carried by one reduction
 constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
 constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
-constexpr int kPolishAttempts = 4;    // active-set corrections
+constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
 constexpr double kPolishDualTol = 1e-7;
 constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
@@ -1699,9 +1699,35 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         block_sum_max_max<kWaves>(unused_a, eres, unused_b, s.sc);  // uniform; also the barrier
         if (eres <= kPolishEqTol * scale_d) break;
       }
-      // sign conditions; violators move (primal-dual active-set step)
+      // sign conditions; violators move (primal-dual active-set step).  Rows that must become
+      // equalities (a dropped row violated, a penalised row with s < 0) and equalities with a
+      // negative multiplier move one per step and attempt, the most violated: moving every
+      // violator at once can leave a step with more binding rows than it has freedom, after which
+      // the multiplier passes diverge and the corrections thrash (degenerate problems).  Every
+      // violator still counts as unresolved.
       double bad = 0.0;
+      {
+        double vmax = 0.0, dmax = 0.0;
+        if (lane < K) {
+          const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+          for (int o = wave; o < O; o += kWaves) {
+            const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
+            const double flag = rows.wA[r];
+            const double hp = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
+            vmax = fmax(vmax, flag == 0.0 ? hp : (flag == 1.0 ? -hp : 0.0));
+            dmax = fmax(dmax, flag == 2.0 ? -rows.s[r] : 0.0);
+          }
+        }
+        s.red[(wave * kPerStepQ) * 64 + lane] = vmax;
+        s.red[(wave * kPerStepQ + 1) * 64 + lane] = dmax;
+      }
+      __syncthreads();
       if (lane < K) {
+        double step_vmax = 0.0, step_dmax = 0.0;
+        for (int w = 0; w < kWaves; ++w) {
+          step_vmax = fmax(step_vmax, s.red[(w * kPerStepQ) * 64 + lane]);
+          step_dmax = fmax(step_dmax, s.red[(w * kPerStepQ + 1) * 64 + lane]);
+        }
         const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
         for (int o = wave; o < O; o += kWaves) {
           const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
@@ -1710,15 +1736,22 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
           double nf = flag, nv = rows.s[r];
           if (flag == 2.0) {
             if (nv > kSlackLin + kPolishDualTol) nf = 1.0;        // the slack is positive after all
-            else if (nv < -kPolishDualTol) nf = 0.0;              // not binding
+            else if (nv < -kPolishDualTol) {                      // not binding (one per step)
+              bad += 1.0;
+              if (-nv >= step_dmax) nf = 0.0;
+            }
             nv = nf == 2.0 ? fmin(fmax(nv, 0.0), kSlackLin) : 0.0;
-          } else if (flag == 1.0) {
-            if (hp < -tolf) { nf = 2.0; nv = 0.0; }               // penalised row with s < 0
-          } else if (hp > tolf) {
-            nf = 2.0;                                             // dropped row violated
-            nv = 0.0;
+            bad += nf == 1.0;
+          } else {
+            const double v = flag == 1.0 ? -hp : hp;              // s < 0 / dropped row violated
+            if (v > tolf) {
+              bad += 1.0;
+              if (v >= step_vmax) {
+                nf = 2.0;
+                nv = 0.0;
+              }
+            }
           }
-          bad += nf != flag;
           rows.wA[r] = nf;
           rows.s[r] = nv;
         }

@@ -29,7 +29,7 @@ for dyn, H, O in [("double", 30, 3), ("double", 32, 6), ("double", 40, 4), ("sin
     u = u.cpu().numpy(); uf = np.concatenate([u1.cpu().numpy(), u2.cpu().numpy()])
     bad = np.nonzero(info[:, 0] != 0)[0]
     badf = np.nonzero(few[:, 0] != 0)[0]
-    print(dyn, H, O, "many-form non-optimal:", bad, info[bad][:, :6] if len(bad) else "", "few-form non-optimal:", badf, "max|du|", np.abs(u - uf).max())
+    print(dyn, H, O, "counts", len(bad), len(badf), "many-form non-optimal:", bad, info[bad][:, :6] if len(bad) else "", "few-form non-optimal:", badf, "max|du|", np.abs(u - uf).max())
     for b in list(bad[:3]):
         xo, uo, io = tm._oracle(probs[b])
         print("  oracle", b, io["status"], "max|u-uo| many", np.abs(u[b] - uo).max(), "few", np.abs(uf[b] - uo).max())
