@@ -37,7 +37,7 @@ METRIC_COLUMNS = {"mean": (_native.COL_MEAN_H0, _native.COL_G_MEAN),
                   "cvar": (_native.COL_H0, _native.COL_G_CVAR),
                   "dr_cvar": (_native.COL_H0, _native.COL_G_DR_TILDE)}
 DEFAULT_MAX_ITER = 60
-DEFAULT_TOL = 1e-10
+DEFAULT_TOL = 1e-8
 
 
 def _bounds(bounds, dim):

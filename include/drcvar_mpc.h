@@ -106,7 +106,7 @@ int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_pr
  *   workspace               drcvar_mpc_workspace_doubles() doubles; per problem it holds eight
  *                           [n_obstacles, 64] arrays h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
  *                           (s = the slack of each halfspace at exit) and the best iterate
- *   max_iter, tol           interior-point limits (e.g. 60, 1e-10); converged when
+ *   max_iter, tol           interior-point limits (e.g. 60, 1e-8); converged when
  *                           max(|r_primal|/(1+|d|), |r_dual|/(1+|q|), mean complementarity) <= tol
  *   polish                  nonzero: finish with the active-set polish (method of multipliers on
  *                           the equality QP of the identified active set, with active-set

@@ -1,0 +1,20 @@
+"""One launch per shape of scripts/mpc_bench.py's problems against DRCVAR_DIAG_LIB (a printf build
+prints the interior-point merit per iteration)."""
+import os
+import sys
+
+sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.join(os.getcwd(), "scripts"))
+import torch  # noqa: E402
+
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf  # noqa: E402
+from mpc_bench import problem_batch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
+    H, O, B = (int(v) for v in shape.split(","))
+    model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
+    print("== shape", shape, flush=True)
+    x, u, info = mf.filter_batch(model, rec[..., 3:5], rec[..., 7], x0, xr, uf)
+    torch.cuda.synchronize()
+    print("info", info[0].cpu().numpy().round(12), flush=True)
