@@ -1443,7 +1443,9 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         amax = fmin(amax, pair_ratio(q, pair_dir(q, l, s.dpa[t], s.dp[t], sigma_mu, true)));
       }
     }
-    const double alpha = fmin(1.0, kStepFrac * block_min<kWaves>(amax, s.sc));
+    // fraction to the boundary: 0.995, closing to 1 - mu near the solution — a fixed 0.995 caps
+    // the tail at a factor-200 reduction per iteration (measured 6e-2, 3e-4, 2e-6, 8e-9, 4e-11)
+    const double alpha = fmin(1.0, (1.0 - fmin(1.0 - kStepFrac, mu)) * block_min<kWaves>(amax, s.sc));
 
     // ---- P5: update (the halfspace rows in the fused pass below) ----
     // this lane's step: positions and directions of the iterate being updated
