@@ -1,3 +1,7 @@
+"""Robustness census of the MPC kernel on the batches of tests/test_mpc.py::
+test_gpu_many_problems_every_form: per shape, the problems that end non-OPTIMAL in the
+many-problem form (one launch of 150) and the few-problem form (launches of <= 128), their info
+records, and the oracle distance of the first few.  GPU only; honours DRCVAR_DIAG_LIB."""
 import sys, os
 sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
 import numpy as np, torch
