@@ -515,8 +515,8 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
     const int i = e / NX, j = e % NX;  // entry (i, j) owned by lane < NX2
     // stage (a) operands held in registers: column j of A (for T) and, for the lanes that also
     // compute U = P B, column c of B
-    const int eu = lane < NX * NU ? lane : 0;
-    const int ui = eu / NU, uc = eu % NU;
+    // U = P B: entry (i, j) for j < NU from the same row of P as T (no second row load)
+    const int uc = j < NU ? j : 0;
     double Acol[NX], Bcol[NX];
 #pragma unroll
     for (int m = 0; m < NX; ++m) {
@@ -552,20 +552,17 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
       wave_lds_fence();
       // (a) T = P A (lane = entry), U = P B (lane = entry of U)
       {
-        double prow[NX], urow[NX];
+        double prow[NX];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) {
-          prow[m] = s.P[i * kMx + m];
-          urow[m] = s.P[ui * kMx + m];
-        }
+        for (int m = 0; m < NX; ++m) prow[m] = s.P[i * kMx + m];
         double t = 0.0, uu = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) {
           t += prow[m] * Acol[m];
-          uu += urow[m] * Bcol[m];
+          uu += prow[m] * Bcol[m];
         }
         if (lane < NX2) s.T[i * kMx + j] = t;
-        if (lane < NX * NU) s.U[ui * NU + uc] = uu;
+        if (lane < NX2 && j < NU) s.U[i * NU + j] = uu;
       }
       wave_lds_fence();
       // (b) every operand in one batch: T columns i and j, U, B, the weights of step k
