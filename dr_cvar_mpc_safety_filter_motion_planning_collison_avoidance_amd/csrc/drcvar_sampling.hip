@@ -54,10 +54,12 @@ __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32
   return Philox{{c0, c1, c2, c3}};
 }
 
-// 53-bit uniform in the open interval (0, 1)
-__device__ __forceinline__ double uniform53(uint32_t hi, uint32_t lo) {
-  const uint64_t v = (static_cast<uint64_t>(hi) << 32 | lo) >> 11;
-  return (static_cast<double>(v) + 0.5) * 0x1.0p-53;
+// Uniform in the open interval (0, 1) from the top 52 bits: (v + 1/2) 2^-52 needs 53 significant
+// bits, so it is exact, and lies in [2^-53, 1 - 2^-53].  (A 53-bit v would round v + 1/2 up to
+// 2^53 for v = 2^53 - 1, i.e. u = 1 and log u = 0 -> rsq(-0) = -inf -> a NaN sample.)
+__device__ __forceinline__ double uniform52(uint32_t hi, uint32_t lo) {
+  const uint64_t v = (static_cast<uint64_t>(hi) << 32 | lo) >> 12;
+  return (static_cast<double>(v) + 0.5) * 0x1.0p-52;
 }
 
 // log(x) for 0 < x <= 1 (normal).  x = m 2^e with m in [sqrt(1/2), sqrt(2)); f = m - 1 is exact;
@@ -92,7 +94,7 @@ __device__ __forceinline__ double log_unit(double x) {
   return fma(de, kLn2Hi, fma(de, kLn2Lo, logm));
 }
 
-// sqrt(-2 log u1).  The argument is >= 2^-53 (u1 <= 1 - 2^-54), never denormal, so rsq + two
+// sqrt(-2 log u1).  The argument is >= 2^-52 (u1 <= 1 - 2^-53), never denormal, so rsq + two
 // Newton-Raphson steps (Goldschmidt form) replace the library sqrt and its rescaling.
 __device__ __forceinline__ double box_muller_radius(double u1) {
   const double y = -2.0 * log_unit(u1);
@@ -136,9 +138,13 @@ __device__ __forceinline__ void cos_sin_turn(uint32_t whi, uint32_t wlo, double*
   *sn = (q & 2) ? -b : b;
 }
 
+// Units [u0, u0 + count) of the global [O, T] grid (u = o T + t); unit u is written at
+// out + (o - o0) so + (t - t0) st with (o0, t0) = divmod(u0, T), so a whole [O, T, N, 2] batch
+// (u0 = 0, any strides) and a flat shard [count, N, 2] (so = T su, st = su) are the same kernel.
 struct SampleArgs {
   const double* nominal;
-  int64_t O, T, N, nom_so, nom_st;
+  int64_t T, N, nom_so, nom_st;
+  int64_t u0, count, o0, t0;
   double l00, l10, l11;
   uint32_t k0, k1, s0, s1;
   int zero_first;
@@ -147,12 +153,12 @@ struct SampleArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
-  const int64_t units = a.O * a.T;
-  for (int64_t u = blockIdx.y; u < units; u += gridDim.y) {
+  for (int64_t k = blockIdx.y; k < a.count; k += gridDim.y) {
+    const int64_t u = a.u0 + k;
     const int64_t o = u / a.T, t = u - o * a.T;
     const double* nom = a.nominal + o * a.nom_so + t * a.nom_st;
     const double nx = nom[0], ny = nom[1];
-    double* dst = a.out + o * a.so + t * a.st;
+    double* dst = a.out + (o - a.o0) * a.so + (t - a.t0) * a.st;
     const bool noise = !(a.zero_first && t == 0);
     const int64_t base = (static_cast<int64_t>(blockIdx.x) * kBlock * kPerThread) + threadIdx.x;
 #pragma unroll
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
         const uint64_t g = static_cast<uint64_t>(u) * static_cast<uint64_t>(a.N) + static_cast<uint64_t>(i);
         const Philox r = philox4x32_10(static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
                                        a.s0, a.s1, a.k0, a.k1);
-        const double rad = box_muller_radius(uniform53(r.x[0], r.x[1]));
+        const double rad = box_muller_radius(uniform52(r.x[0], r.x[1]));
         double sn, cs;
         cos_sin_turn(r.x[2], r.x[3], &cs, &sn);
         const double z0 = rad * cs, z1 = rad * sn;
@@ -182,27 +188,32 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
   }
 }
 
-}  // namespace
 
-extern "C" int drcvar_sample_trajectories_f64(const double* nominal, int64_t n_obstacles,
-                                              int64_t n_steps, int64_t nom_so, int64_t nom_st,
-                                              int64_t n_samples, double l00, double l10, double l11,
-                                              uint64_t seed, uint64_t stream_offset,
-                                              int32_t zero_first_step, double* out, int64_t so,
-                                              int64_t st, int64_t sn, void* stream) {
-  if (n_obstacles < 0 || n_steps < 0 || n_samples < 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+int launch_samples(const double* nominal, int64_t n_obstacles, int64_t n_steps, int64_t nom_so,
+                   int64_t nom_st, int64_t u0, int64_t count, int64_t n_samples, double l00,
+                   double l10, double l11, uint64_t seed, uint64_t stream_offset,
+                   int32_t zero_first_step, double* out, int64_t so, int64_t st, int64_t sn,
+                   void* stream) {
+  if (n_obstacles < 0 || n_steps < 0 || n_samples < 0 || u0 < 0 || count < 0)
+    return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (n_samples > (int64_t{1} << 40) || n_obstacles > (int64_t{1} << 40) ||
+      n_steps > (int64_t{1} << 40) || n_obstacles * n_steps > (int64_t{1} << 40))
+    return DRCVAR_ERR_UNSUPPORTED;
   const int64_t units = n_obstacles * n_steps;
-  if (units == 0 || n_samples == 0) return DRCVAR_OK;
+  if (u0 > units || count > units - u0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (count == 0 || n_samples == 0) return DRCVAR_OK;
   if (!nominal || !out) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (!(l00 == l00) || !(l10 == l10) || !(l11 == l11)) return DRCVAR_ERR_INVALID_ARGUMENT;
-  if (n_samples > (int64_t{1} << 40) || units > (int64_t{1} << 40)) return DRCVAR_ERR_UNSUPPORTED;
   SampleArgs a{};
   a.nominal = nominal;
-  a.O = n_obstacles;
   a.T = n_steps;
   a.N = n_samples;
   a.nom_so = nom_so;
   a.nom_st = nom_st;
+  a.u0 = u0;
+  a.count = count;
+  a.o0 = u0 / n_steps;
+  a.t0 = u0 - a.o0 * n_steps;
   a.l00 = l00;
   a.l10 = l10;
   a.l11 = l11;
@@ -218,9 +229,38 @@ extern "C" int drcvar_sample_trajectories_f64(const double* nominal, int64_t n_o
   const int64_t per_block = int64_t{kBlock} * kPerThread;
   const int64_t gx = (n_samples + per_block - 1) / per_block;
   if (gx > 0x7fffffffLL) return DRCVAR_ERR_UNSUPPORTED;
-  const unsigned gy = static_cast<unsigned>(units < 65535 ? units : 65535);
+  const unsigned gy = static_cast<unsigned>(count < 65535 ? count : 65535);
   (void)hipGetLastError();
   hipLaunchKernelGGL(sample_kernel, dim3(static_cast<unsigned>(gx), gy), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
+}
+
+}  // namespace
+
+extern "C" int drcvar_sample_trajectories_f64(const double* nominal, int64_t n_obstacles,
+                                              int64_t n_steps, int64_t nom_so, int64_t nom_st,
+                                              int64_t n_samples, double l00, double l10, double l11,
+                                              uint64_t seed, uint64_t stream_offset,
+                                              int32_t zero_first_step, double* out, int64_t so,
+                                              int64_t st, int64_t sn, void* stream) {
+  if (n_obstacles < 0 || n_steps < 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (n_obstacles > (int64_t{1} << 40) || n_steps > (int64_t{1} << 40)) return DRCVAR_ERR_UNSUPPORTED;
+  return launch_samples(nominal, n_obstacles, n_steps, nom_so, nom_st, 0, n_obstacles * n_steps,
+                        n_samples, l00, l10, l11, seed, stream_offset, zero_first_step, out, so, st,
+                        sn, stream);
+}
+
+extern "C" int drcvar_sample_units_f64(const double* nominal, int64_t n_obstacles, int64_t n_steps,
+                                       int64_t nom_so, int64_t nom_st, int64_t unit_begin,
+                                       int64_t unit_count, int64_t n_samples, double l00,
+                                       double l10, double l11, uint64_t seed,
+                                       uint64_t stream_offset, int32_t zero_first_step,
+                                       double* out, int64_t su, int64_t sn, void* stream) {
+  if (n_steps <= 0 && unit_count > 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (n_steps > (int64_t{1} << 40) || su > (int64_t{1} << 40)) return DRCVAR_ERR_UNSUPPORTED;
+  // (o - o0) T su + (t - t0) su = (u - u0) su
+  return launch_samples(nominal, n_obstacles, n_steps, nom_so, nom_st, unit_begin, unit_count,
+                        n_samples, l00, l10, l11, seed, stream_offset, zero_first_step, out,
+                        n_steps * su, su, sn, stream);
 }

@@ -78,6 +78,19 @@ def _check_pairs(t: torch.Tensor, name: str, rows: int, device: torch.device) ->
                          f"{tuple(t.shape)}")
 
 
+def _check_out(out, shape, device: torch.device, what: str) -> None:
+    """A caller-supplied output buffer must be exactly what the kernel writes: the engine writes
+    ``prod(shape) * 8`` doubles through the raw pointer, so anything else is an out-of-bounds
+    device write (checked before any ABI call)."""
+    if not isinstance(out, torch.Tensor):
+        raise TypeError("out must be a torch.Tensor")
+    if (tuple(out.shape) != tuple(shape) or out.dtype != torch.float64 or not out.is_contiguous()
+            or out.device != device):
+        raise ValueError(f"out must be a contiguous float64 {what} tensor on {device}, got "
+                         f"{tuple(out.shape)} {out.dtype} on {out.device}"
+                         f"{'' if out.is_contiguous() else ' (non-contiguous)'}")
+
+
 def _typed(args):
     """Pre-convert an argument tuple to ctypes objects (saves the per-call conversion)."""
     out = []
@@ -118,9 +131,8 @@ def prepare_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: Ri
     _check_pairs(ego, "ego", T, samples.device)
     if out is None:
         out = torch.empty((O, T, OUT_WIDTH), dtype=torch.float64, device=samples.device)
-    elif (out.shape != (O, T, OUT_WIDTH) or out.dtype != torch.float64 or not out.is_contiguous()
-          or out.device != samples.device):
-        raise ValueError("out must be a contiguous float64 [O, T, 8] tensor on the samples' device")
+    else:
+        _check_out(out, (O, T, OUT_WIDTH), samples.device, "[O, T, 8]")
     lib = _native.lib()
     so, st, sn = samples.stride(0), samples.stride(1), samples.stride(2)
     args = (ctypes.c_void_p(samples.data_ptr()), O, T, N, so, st, sn,
@@ -159,6 +171,8 @@ def offsets_given_h(samples: torch.Tensor, h: torch.Tensor, params: RiskParams =
     _check_pairs(h, "h", U, samples.device)
     if out is None:
         out = torch.empty((U, OUT_WIDTH), dtype=torch.float64, device=samples.device)
+    else:
+        _check_out(out, (U, OUT_WIDTH), samples.device, "[U, 8]")
     if U == 0:
         return out
     lib = _native.lib()

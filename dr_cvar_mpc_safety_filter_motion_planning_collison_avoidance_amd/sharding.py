@@ -1,15 +1,29 @@
 """Multi-GPU sharding of the (obstacle x step) unit batch — one process per GPU.
 
 Units are independent (no cross-unit data in ``core/halfspaces.py:225-246`` or
-``simulation/environment.py:82-104``), so the batch is split into contiguous blocks of the
-flattened unit index ``u = o*T + t`` with no data-path collective.  The only exchange is the one
-the consumer needs: the MPC QP (``core/mpc_filter.py:116-144``) takes every halfspace of the
-horizon, so :func:`gather_records` reassembles the ``[U, 8]`` records on every rank with ONE
-``all_gather_into_tensor`` (RCCL over xGMI when the backend is ``nccl``; gloo in the CPU tests).
-Each record is 64 B, so even the largest config (12 800 units, 800 KB) is latency-bound.
+``simulation/environment.py:82-104``), so the flattened unit index ``u = o*T + t`` is split into
+contiguous blocks (:func:`shard_bounds`) and each rank evaluates its block with no data-path
+collective.  The only exchange is the one the consumer needs: the MPC QP
+(``core/mpc_filter.py:116-144``) takes every halfspace of the horizon, so the ``[U, 8]`` records
+are reassembled on every rank with ONE ``all_gather_into_tensor`` (RCCL over xGMI when the
+backend is ``nccl``; gloo in the CPU tests).  A record is 64 B, so even the largest config
+(12 800 units, 800 KB) is a latency-bound exchange.
 
-``compute`` is injectable so the partition/gather logic can be exercised with world_size 2 on
-CPU (gloo) in the tests; the product path always passes the HIP engine.
+Two forms:
+
+* :func:`sharded_safe_halfspaces` — the global ``[O, T, N, 2]`` batch exists on every rank (e.g.
+  the reference's harness handed it over); a rank's block is addressed through at most three
+  strided VIEWS of it (:func:`shard_views`: the tail of one obstacle, whole obstacles, the head of
+  another), never a copy, whatever the batch's strides.
+* :class:`ShardedBatch` — the global batch exists on NO rank: each rank draws only its own units
+  with the device sampler (``drcvar_sample_units_f64``, the same Philox counters the whole batch
+  would use), the kernel writes straight into its slice of the all-gather input, and
+  :meth:`ShardedBatch.step` is one launch + one ``all_gather_into_tensor``.  This is the
+  north-star multi-GPU form ``bench.py`` times.
+
+``compute`` is injectable in :func:`sharded_safe_halfspaces` so the partition/gather logic can be
+exercised with world_size 2 on CPU (gloo) in the tests; the product path always passes the HIP
+engine.
 """
 from __future__ import annotations
 
@@ -30,45 +44,154 @@ def shard_bounds(n_units: int, world_size: int, rank: int) -> tuple[int, int]:
     return start, min(start + per, n_units)
 
 
-def shard_units(samples: torch.Tensor, ego: torch.Tensor, world_size: int, rank: int):
-    """This rank's units of an [O, T, N, 2] batch, flattened: ``(samples [u, N, 2], ego [u, 2],
-    start, stop)``.  Works on any device; no copy of the samples when they are contiguous."""
-    O, T, N, _ = samples.shape
+def shard_pieces(n_obstacles: int, n_steps: int, start: int, stop: int):
+    """Split the unit block ``[start, stop)`` of an ``[O, T]`` grid into at most three rectangles
+    ``(o_lo, o_hi, t_lo, t_hi, offset)`` — the rest of one obstacle's steps, whole obstacles, the
+    first steps of one more — each a strided view of any ``[O, T, ...]`` tensor; ``offset`` is
+    the rectangle's first unit relative to ``start``."""
+    O, T = n_obstacles, n_steps
+    if not (0 <= start <= stop <= O * T):
+        raise ValueError(f"unit block [{start}, {stop}) outside the {O} x {T} grid")
+    pieces, u = [], start
+    while u < stop:
+        o, t = divmod(u, T)
+        if t or stop - u < T:                       # a partial obstacle row
+            t_hi = min(T, t + stop - u)
+            pieces.append((o, o + 1, t, t_hi, u - start))
+            u += t_hi - t
+        else:                                       # whole obstacles
+            n = (stop - u) // T
+            pieces.append((o, o + n, 0, T, u - start))
+            u += n * T
+    return pieces
+
+
+def shard_views(samples: torch.Tensor, ego: torch.Tensor, world_size: int, rank: int):
+    """This rank's units of an ``[O, T, N, 2]`` batch (any strides) as strided views:
+    ``([(samples [o, t, N, 2], ego [t, 2], offset, count)], start, stop)`` — no copies."""
+    O, T = samples.shape[:2]
     start, stop = shard_bounds(O * T, world_size, rank)
-    flat = samples.reshape(O * T, N, 2)
-    ego_units = ego.repeat(O, 1)  # unit u -> ego[u % T]
-    return flat[start:stop], ego_units[start:stop], start, stop
+    views = [(samples[o0:o1, t0:t1], ego[t0:t1], off, (o1 - o0) * (t1 - t0))
+             for o0, o1, t0, t1, off in shard_pieces(O, T, start, stop)]
+    return views, start, stop
 
 
-def engine_compute(samples_u: torch.Tensor, ego_u: torch.Tensor, params: RiskParams) -> torch.Tensor:
-    """HIP engine on a flattened shard: [u, N, 2] x [u, 2] -> [u, 8] (one launch)."""
-    u = samples_u.shape[0]
-    if u == 0:
-        return torch.empty((0, engine.OUT_WIDTH), dtype=torch.float64, device=samples_u.device)
-    # one obstacle row with u steps, ego per step = ego per unit
-    return engine.safe_halfspaces(samples_u.unsqueeze(0), ego_u, params).reshape(u, engine.OUT_WIDTH)
+def engine_compute(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams,
+                   out: torch.Tensor) -> None:
+    """HIP engine on one rectangle: ``[o, t, N, 2]`` x ``[t, 2]`` -> ``out [o, t, 8]`` (one launch,
+    strided samples consumed in place)."""
+    engine.safe_halfspaces(samples, ego, params, out=out)
 
 
-def gather_records(local: torch.Tensor, n_units: int, group=None) -> torch.Tensor:
-    """All-gather every rank's ``[u_r, 8]`` block into the full ``[n_units, 8]`` on every rank."""
+def _all_gather(full: torch.Tensor, send: torch.Tensor, group=None) -> None:
+    if full.device == send.device:
+        dist.all_gather_into_tensor(full, send, group=group)
+    else:                                           # gloo rehearsal of device records
+        host = torch.empty_like(full, device=full.device)
+        dist.all_gather_into_tensor(host, send.to(full.device), group=group)
+        full.copy_(host)
+
+
+def gather_records(send: torch.Tensor, n_units: int, group=None) -> torch.Tensor:
+    """All-gather every rank's padded ``[ceil(U/W), 8]`` block into ``[n_units, 8]`` on every
+    rank (one collective; the padding rows of the tail rank are dropped)."""
     world = dist.get_world_size(group)
-    per = -(-n_units // world) if n_units else 0
-    padded = torch.zeros((per, local.shape[1]), dtype=local.dtype, device=local.device)
-    padded[: local.shape[0]] = local
-    full = torch.empty((per * world, local.shape[1]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(full, padded, group=group)
+    full = torch.empty((send.shape[0] * world, send.shape[1]), dtype=send.dtype, device=send.device)
+    dist.all_gather_into_tensor(full, send, group=group)
     return full[:n_units]
 
 
 def sharded_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams,
                             group=None, gather: bool = True, compute=engine_compute):
-    """Evaluate this rank's share of an [O, T, N, 2] batch; with ``gather`` return the full
-    [O, T, 8] record on every rank, else ``(local [u, 8], start, stop)``."""
+    """Evaluate this rank's share of an ``[O, T, N, 2]`` batch; with ``gather`` return the full
+    ``[O, T, 8]`` record on every rank, else ``(local [u, 8], start, stop)``."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     O, T = samples.shape[:2]
-    s_u, e_u, start, stop = shard_units(samples, ego, world, rank)
-    local = compute(s_u, e_u, params)
+    views, start, stop = shard_views(samples, ego, world, rank)
+    per = -(-(O * T) // world) if O * T else 0
+    send = torch.zeros((per, engine.OUT_WIDTH), dtype=torch.float64, device=samples.device)
+    for s, e, off, cnt in views:
+        compute(s, e, params, send[off:off + cnt].view(s.shape[0], s.shape[1], engine.OUT_WIDTH))
     if not gather:
-        return local, start, stop
-    return gather_records(local, O * T, group).reshape(O, T, -1)
+        return send[:stop - start], start, stop
+    return gather_records(send, O * T, group).reshape(O, T, engine.OUT_WIDTH)
+
+
+class ShardedBatch:
+    """One rank's block of a global ``[O, T, N, 2]`` obstacle-sample batch that no rank holds.
+
+    ``nominal [O, T, 2]`` / ``ego [T, 2]`` describe the global batch (tiny; identical on every
+    rank).  The rank's units ``[start, stop)`` are drawn once on its device
+    (``drcvar_sample_units_f64``: sample for sample what the whole batch would hold), laid out flat
+    ``[count, N, 2]`` and evaluated as ONE launch of a ``[1, count]`` grid whose per-unit ego is
+    ``ego[u mod T]``.  The kernel writes into ``send[:count]``, the all-gather input itself; with
+    ``world > 1`` :meth:`step` then runs ``all_gather_into_tensor(full, send)`` — on RCCL the
+    records go device to device, nothing is staged.  ``records()`` is the global ``[O, T, 8]``.
+    """
+
+    def __init__(self, nominal: torch.Tensor, ego: torch.Tensor, n_samples: int, params: RiskParams,
+                 world_size: int = 1, rank: int = 0, group=None, seed: int = 42,
+                 stream_offset: int = 0, noise_cov=None, zero_first_step: bool = True,
+                 gather_device=None):
+        from .simulation import obstacles
+        O, T = int(nominal.shape[0]), int(nominal.shape[1])
+        dev = nominal.device
+        self.O, self.T, self.N = O, T, int(n_samples)
+        self.U = O * T
+        self.world, self.rank, self.group = world_size, rank, group
+        self.params = params
+        self.start, self.stop = shard_bounds(self.U, world_size, rank)
+        self.count = self.stop - self.start
+        self.per = -(-self.U // world_size) if self.U else 0
+        cov = obstacles.NOISE_COV if noise_cov is None else noise_cov
+        self.samples = obstacles.sample_units_device(nominal, self.N, self.start, self.count, cov,
+                                                     seed=seed, stream_offset=stream_offset,
+                                                     zero_first_step=zero_first_step)
+        idx = torch.arange(self.start, self.stop, device=dev) % T
+        self.ego_units = ego.index_select(0, idx).contiguous()            # [count, 2], built once
+        self.send = torch.zeros((self.per, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
+        gdev = dev if gather_device is None else torch.device(gather_device)
+        self.full = (torch.empty((self.per * world_size, engine.OUT_WIDTH), dtype=torch.float64,
+                                 device=gdev) if world_size > 1 else None)
+        self._launch = self.prepare()
+
+    def prepare(self, stream=None):
+        """A frozen launch of this rank's block on ``stream`` (default: the current stream) — for
+        hipGraph capture pass the capturing stream."""
+        if self.count == 0:
+            return None
+        launch, _ = engine.prepare_safe_halfspaces(
+            self.samples.unsqueeze(0), self.ego_units, self.params,
+            out=self.send[:self.count].view(1, self.count, engine.OUT_WIDTH), stream=stream)
+        return launch
+
+    def compute(self, launch=None) -> None:
+        """The halfspace kernel over this rank's units (no collective)."""
+        launch = launch if launch is not None else self._launch
+        if launch is not None:
+            launch()
+
+    def exchange(self) -> None:
+        """The QP hand-off exchange: every rank's records to every rank (no-op at world 1)."""
+        if self.full is not None:
+            _all_gather(self.full, self.send, self.group)
+
+    def step(self, launch=None) -> None:
+        self.compute(launch)
+        self.exchange()
+
+    def local_records(self) -> torch.Tensor:
+        """``[count, 8]`` records of this rank's units (a view of the all-gather input)."""
+        return self.send[:self.count]
+
+    def records(self) -> torch.Tensor:
+        """Global ``[O, T, 8]`` records (after :meth:`step`; at world 1 the local block)."""
+        src = self.full if self.full is not None else self.send
+        return src[:self.U].view(self.O, self.T, engine.OUT_WIDTH)
+
+    @property
+    def algorithmic_bytes(self) -> int:
+        """Bytes this rank's launch must move: its samples once, a 64-B record and the ego pair
+        per unit (the ego is per unit here: ``[count, 2]``)."""
+        return self.count * (16 * self.N + 64 + 16)

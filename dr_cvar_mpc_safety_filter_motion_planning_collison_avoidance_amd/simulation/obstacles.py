@@ -120,6 +120,41 @@ def sample_trajectories_device(nominal, n_samples, noise_cov=NOISE_COV, seed=0, 
     return out
 
 
+def sample_units_device(nominal, n_samples, unit_begin, unit_count, noise_cov=NOISE_COV, seed=0,
+                        stream_offset=0, zero_first_step=True, out=None, stream=None):
+    """Units ``[unit_begin, unit_begin + unit_count)`` of the global batch ``nominal`` ``[O, T, 2]``
+    describes, as a flat ``[unit_count, N, 2]`` float64 device tensor (unit ``u = o * T + t``).
+
+    Sample for sample the same values :func:`sample_trajectories_device` draws for the whole batch
+    (``drcvar_sample_units_f64``): one rank draws its shard of a global batch and nothing else.
+    ``out`` may be any ``[unit_count, N, 2]`` view with adjacent coordinates.
+    """
+    if not isinstance(nominal, torch.Tensor) or nominal.device.type != "cuda":
+        raise ValueError("nominal must be a device tensor (the sampler has no CPU path)")
+    if nominal.dtype != torch.float64 or nominal.dim() != 3 or nominal.shape[2] != 2 or \
+            nominal.stride(2) != 1:
+        raise ValueError("nominal must be float64 [O, T, 2] with adjacent coordinates")
+    O, T, _ = nominal.shape
+    unit_begin, unit_count, n_samples = int(unit_begin), int(unit_count), int(n_samples)
+    if unit_begin < 0 or unit_count < 0 or unit_begin + unit_count > O * T:
+        raise ValueError(f"unit range [{unit_begin}, {unit_begin + unit_count}) outside the "
+                         f"{O} x {T} batch")
+    L = np.linalg.cholesky(np.asarray(noise_cov, dtype=np.float64).reshape(2, 2))
+    if out is None:
+        out = torch.empty((unit_count, n_samples, 2), dtype=torch.float64, device=nominal.device)
+    elif tuple(out.shape) != (unit_count, n_samples, 2) or out.dtype != torch.float64 or \
+            out.stride(2) != 1 or out.device != nominal.device:
+        raise ValueError("out must be a float64 [units, N, 2] device view with adjacent coordinates")
+    s = stream if stream is not None else torch.cuda.current_stream(nominal.device)
+    _native.check(_native.lib().drcvar_sample_units_f64(
+        ctypes.c_void_p(nominal.data_ptr()), O, T, nominal.stride(0), nominal.stride(1),
+        unit_begin, unit_count, n_samples, float(L[0, 0]), float(L[1, 0]), float(L[1, 1]),
+        ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), ctypes.c_uint64(int(stream_offset) & (2 ** 64 - 1)),
+        1 if zero_first_step else 0, ctypes.c_void_p(out.data_ptr()), out.stride(0), out.stride(1),
+        ctypes.c_void_p(int(s.cuda_stream))))
+    return out
+
+
 def generate_obstacle_scenarios_device(scenario_config, horizon, dt, n_samples=100, seed=0,
                                        device=None):
     """``generate_obstacle_scenarios`` with the samples drawn on the device.

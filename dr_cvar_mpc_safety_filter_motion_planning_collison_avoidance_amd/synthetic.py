@@ -36,8 +36,9 @@ def straight_line_ego(n_steps: int, device, start=(-4.0, 0.0), goal=(4.0, 0.0), 
     return ego.to(device)
 
 
-def obstacle_batch(n_obstacles: int, n_steps: int, n_samples: int, device, seed: int = 42):
-    """(samples [O, T, N, 2] f64, ego [T, 2] f64) on ``device``, deterministic for a seed."""
+def nominal_paths(n_obstacles: int, n_steps: int, device, seed: int = 42) -> torch.Tensor:
+    """Nominal obstacle positions ``[O, T, 2]`` f64 on ``device`` (deterministic for a seed): start
+    ~ U[-5, 5]^2, heading ~ U[0, 2 pi), speed ~ U[0.6, 1.5] m/s, straight lines at DT."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     f64 = dict(dtype=torch.float64, device=device)
@@ -46,7 +47,15 @@ def obstacle_batch(n_obstacles: int, n_steps: int, n_samples: int, device, seed:
     speed = 0.6 + torch.rand((n_obstacles,), generator=g, **f64) * 0.9
     vel = torch.stack([torch.cos(heading), torch.sin(heading)], dim=1) * speed[:, None]
     t = torch.arange(n_steps, **f64) * DT
-    nominal = (start[:, None, :] + t[None, :, None] * vel[:, None, :]).contiguous()   # [O, T, 2]
-    samples = sample_trajectories_device(nominal, n_samples, [[NOISE_STD ** 2, 0.0], [0.0, NOISE_STD ** 2]],
-                                         seed=seed, zero_first_step=True)             # obstacles.py:63
+    return (start[:, None, :] + t[None, :, None] * vel[:, None, :]).contiguous()
+
+
+NOISE_COV = [[NOISE_STD ** 2, 0.0], [0.0, NOISE_STD ** 2]]
+
+
+def obstacle_batch(n_obstacles: int, n_steps: int, n_samples: int, device, seed: int = 42):
+    """(samples [O, T, N, 2] f64, ego [T, 2] f64) on ``device``, deterministic for a seed."""
+    nominal = nominal_paths(n_obstacles, n_steps, device, seed)
+    samples = sample_trajectories_device(nominal, n_samples, NOISE_COV, seed=seed,
+                                         zero_first_step=True)                       # obstacles.py:63
     return samples, straight_line_ego(n_steps, device)

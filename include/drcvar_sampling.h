@@ -11,9 +11,11 @@
  *   drcvar_sample_trajectories_f64   replaces simulation/obstacles.py:43-77 (and the per-obstacle
  *                                    loop of generate_obstacle_scenarios, :150-163) for a batch
  *                                    of obstacles.
+ *   drcvar_sample_units_f64          the same draws for a contiguous block of (obstacle, step)
+ *                                    units of a global batch (one rank's shard).
  *
  * Random numbers: Philox4x32-10 (counter-based; key = seed, counter = (sample index, stream)),
- * one call per sample -> two 53-bit uniforms -> Box-Muller -> z ~ N(0, I2); sample = nominal +
+ * one call per sample -> a 52-bit uniform and a 64-bit turn -> Box-Muller -> z ~ N(0, I2); sample = nominal +
  * L z with L the lower Cholesky factor of noise_cov.  Same distribution as the reference's
  * np.random.multivariate_normal, not the same stream (numpy's MT19937 is sequential; the host
  * mirror in simulation/obstacles.py reproduces that stream exactly).  Output is a pure function
@@ -46,6 +48,20 @@ int drcvar_sample_trajectories_f64(const double* nominal, int64_t n_obstacles, i
                                    double l10, double l11, uint64_t seed, uint64_t stream_offset,
                                    int32_t zero_first_step, double* out, int64_t so, int64_t st,
                                    int64_t sn, void* stream);
+
+/*
+ * Units [unit_begin, unit_begin + unit_count) of the global [n_obstacles, n_steps] grid (unit
+ * u = o * n_steps + t), written flat: unit u at out + (u - unit_begin) * su, sample i at + i * sn.
+ * Every sample is the one drcvar_sample_trajectories_f64 draws for the whole grid (same Philox
+ * counter u * n_samples + i), so a rank can draw its shard of a global batch without the rest
+ * (per-rank sampling of contiguous unit blocks).  nominal is the GLOBAL
+ * [n_obstacles, n_steps, 2] path.
+ */
+int drcvar_sample_units_f64(const double* nominal, int64_t n_obstacles, int64_t n_steps,
+                            int64_t nom_so, int64_t nom_st, int64_t unit_begin, int64_t unit_count,
+                            int64_t n_samples, double l00, double l10, double l11, uint64_t seed,
+                            uint64_t stream_offset, int32_t zero_first_step, double* out,
+                            int64_t su, int64_t sn, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,7 @@ global index ``g = (o * T + t) * N + i``
 
 * Philox4x32-10 (Salmon et al., SC'11; multipliers 0xD2511F53 / 0xCD9E8D57, Weyl key increments
   0x9E3779B9 / 0xBB67AE85) on counter ``(g lo, g hi, stream lo, stream hi)`` and key ``seed``;
-* ``u1 = ((x0:x1) >> 11 + 1/2) / 2^53`` in (0, 1); angle ``2 pi (x2:x3) / 2^64``;
+* ``u1 = ((x0:x1) >> 12 + 1/2) / 2^52`` in (0, 1) (exact); angle ``2 pi (x2:x3) / 2^64``;
 * Box-Muller ``z = sqrt(-2 log u1) (cos, sin)``; sample ``nominal + L z``.
 
 ``log_unit`` and ``cos_sin_turn`` restate the kernel's own series (atanh series of
@@ -43,9 +43,10 @@ def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
     return c0, c1, c2, c3
 
 
-def uniform53(hi, lo):
-    v = ((hi << np.uint64(32)) | lo) >> np.uint64(11)
-    return (v.astype(np.float64) + 0.5) * 2.0 ** -53
+def uniform52(hi, lo):
+    """(top 52 bits + 1/2) / 2^52: exact, in [2^-53, 1 - 2^-53] (the kernel's ``uniform52``)."""
+    v = ((hi << np.uint64(32)) | lo) >> np.uint64(12)
+    return (v.astype(np.float64) + 0.5) * 2.0 ** -52
 
 
 def log_unit(x):
@@ -100,7 +101,7 @@ def sample_trajectories(nominal, n_samples: int, chol, seed: int, stream_offset:
                                    np.uint64(stream_offset & 0xFFFFFFFF),
                                    np.uint64((stream_offset >> 32) & 0xFFFFFFFF),
                                    seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    rad = np.sqrt(-2.0 * log_unit(uniform53(x0, x1)))
+    rad = np.sqrt(-2.0 * log_unit(uniform52(x0, x1)))
     cs, sn = cos_sin_turn(x2, x3)
     z0, z1 = rad * cs, rad * sn
     out = np.empty((O, T, n_samples, 2))

@@ -20,15 +20,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _oracle_compute(samples_u, ego_u, p):
+def _oracle_compute(samples, ego, p, out):
     from oracle import c_oracle
-    u = samples_u.shape[0]
-    out = c_oracle.safe_halfspaces(samples_u.numpy()[None], ego_u.numpy(), p.robot_radius,
-                                   p.obstacle_radius, p.alpha, p.delta, p.epsilon)
-    return torch.from_numpy(out.reshape(u, 8))
+    out.copy_(torch.from_numpy(c_oracle.safe_halfspaces(
+        samples.contiguous().numpy(), ego.contiguous().numpy(), p.robot_radius, p.obstacle_radius,
+        p.alpha, p.delta, p.epsilon)))
 
 
-def _worker(rank, world, port, O, T, N, q):
+def _worker(rank, world, port, O, T, N, strided, q):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -37,6 +36,8 @@ def _worker(rank, world, port, O, T, N, q):
         rng = np.random.default_rng(42)
         samples = torch.from_numpy(rng.normal(size=(O, T, N, 2)))
         ego = torch.from_numpy(rng.normal(size=(T, 2)))
+        if strided:   # the reference's own [O, N, T, 2] order, consumed through views
+            samples = samples.permute(0, 2, 1, 3).contiguous().permute(0, 2, 1, 3)
         full = sharding.sharded_safe_halfspaces(samples, ego, RiskParams(), compute=_oracle_compute)
         local, a, b = sharding.sharded_safe_halfspaces(samples, ego, RiskParams(), gather=False,
                                                        compute=_oracle_compute)
@@ -45,13 +46,14 @@ def _worker(rank, world, port, O, T, N, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("O,T,N", [(3, 5, 40), (1, 3, 17), (10, 20, 100)])
-def test_two_rank_gather_matches_single_process(O, T, N):
+@pytest.mark.parametrize("O,T,N,strided", [(3, 5, 40, False), (1, 3, 17, False), (10, 20, 100, False),
+                                           (3, 5, 40, True), (5, 3, 12, True)])
+def test_two_rank_gather_matches_single_process(O, T, N, strided):
     from oracle import c_oracle
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, O, T, N, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, O, T, N, strided, q)) for r in range(2)]
     for p in procs:
         p.start()
     results = [q.get(timeout=120) for _ in procs]

@@ -51,12 +51,34 @@ def test_shard_bounds_partition(units, world):
     assert all(b - a <= per for a, b in spans)
 
 
-def test_shard_units_ego_mapping():
-    O, T, N = 3, 5, 4
-    s = torch.arange(O * T * N * 2, dtype=torch.float64).reshape(O, T, N, 2)
+@pytest.mark.parametrize("O,T,world", [(3, 5, 4), (1, 7, 3), (4, 4, 2), (2, 3, 8), (5, 1, 2), (256, 50, 8)])
+def test_shard_views_are_views_and_map_units(O, T, world):
+    """Each rank's block is at most three strided views of the global tensor (never a copy, even
+    for the reference's permuted [O, N, T, 2] order) and covers exactly units [start, stop)."""
+    N = 3
+    base = torch.arange(O * T * N * 2, dtype=torch.float64)
+    layouts = [base.reshape(O, T, N, 2), base.reshape(O, N, T, 2).permute(0, 2, 1, 3)]
     ego = torch.arange(T * 2, dtype=torch.float64).reshape(T, 2)
-    for r in range(4):
-        su, eu, a, b = sharding.shard_units(s, ego, 4, r)
-        for k, u in enumerate(range(a, b)):
-            assert torch.equal(su[k], s[u // T, u % T])
-            assert torch.equal(eu[k], ego[u % T])
+    for s in layouts:
+        seen = []
+        for r in range(world):
+            views, a, b = sharding.shard_views(s, ego, world, r)
+            assert len(views) <= 3
+            assert sum(c for *_, c in views) == b - a
+            for sv, ev, off, cnt in views:
+                assert sv.untyped_storage().data_ptr() == s.untyped_storage().data_ptr()
+                o_n, t_n = sv.shape[:2]
+                assert o_n * t_n == cnt and sv.shape[2:] == (N, 2)
+                for k in range(cnt):
+                    u = a + off + k
+                    assert torch.equal(sv[k // t_n, k % t_n], s[u // T, u % T])
+                    assert torch.equal(ev[k % t_n], ego[u % T])
+                    seen.append(u)
+        assert seen == list(range(O * T))
+
+
+def test_shard_pieces_rejects_bad_blocks():
+    with pytest.raises(ValueError):
+        sharding.shard_pieces(2, 3, 4, 7)
+    assert sharding.shard_pieces(2, 3, 2, 2) == []
+    assert sharding.shard_pieces(4, 5, 3, 17) == [(0, 1, 3, 5, 0), (1, 3, 0, 5, 2), (3, 4, 0, 2, 12)]

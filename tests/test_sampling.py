@@ -71,7 +71,7 @@ def test_sampler_series_accuracy():
     rng = np.random.default_rng(3)
     v = rng.integers(0, 2 ** 53, size=400_000, dtype=np.uint64)
     u = np.concatenate([(v.astype(np.float64) + 0.5) * 2.0 ** -53,
-                        [2.0 ** -54, 1 - 2.0 ** -53, 0.5, 0.25, 0.7071067811865475, 0.7071067811865476]])
+                        [2.0 ** -54, 1 - 2.0 ** -53, 2.0 ** -53, 0.5, 0.25, 0.7071067811865475, 0.7071067811865476]])
     ref = np.log(u.astype(np.longdouble))
     ulp = np.spacing(np.abs(ref.astype(np.float64)))
     assert np.max(np.abs(ps.log_unit(u) - ref) / ulp) <= 2.0
@@ -83,6 +83,19 @@ def test_sampler_series_accuracy():
     th = (w53.astype(np.longdouble) / np.longdouble(2.0 ** 64)) * (2 * pi)
     assert np.max(np.abs(c - np.cos(th))) < 4e-16 and np.max(np.abs(s - np.sin(th))) < 4e-16
     assert np.allclose(c * c + s * s, 1.0, atol=5e-16, rtol=0)
+
+
+def test_uniform_open_interval_extremes():
+    """ADVICE r1: the all-ones word must not map to u = 1 (log 1 = 0 -> a NaN Box-Muller radius);
+    the 52-bit uniform is exact and stays in [2^-53, 1 - 2^-53]."""
+    from oracle import philox_sampler as ps
+    ones, zero = np.array([0xFFFFFFFF], dtype=np.uint64), np.array([0], dtype=np.uint64)
+    hi = ps.uniform52(ones, ones)[0]
+    lo = ps.uniform52(zero, zero)[0]
+    assert hi == 1.0 - 2.0 ** -53 and lo == 2.0 ** -53
+    for u in (hi, lo):
+        r = np.sqrt(-2.0 * ps.log_unit(np.array([u])))[0]
+        assert np.isfinite(r) and r > 0
 
 
 @pytest.fixture(scope="module")
@@ -173,3 +186,35 @@ def test_device_scenario_feeds_the_engine(dev):
     ref = c_oracle.safe_halfspaces(samples.contiguous().cpu().numpy(), ego.cpu().numpy(),
                                    0.3, 0.3, 0.2, 0.1, 0.15)
     assert np.max(np.abs(rec - ref)) < OFFSET_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("O,T,N,begin,count", [(4, 5, 300, 0, 20), (4, 5, 300, 3, 9), (4, 5, 300, 7, 13),
+                                               (3, 7, 1000, 20, 1), (2, 3, 1, 1, 4), (5, 4, 64, 6, 0)])
+def test_device_sampler_unit_range_is_a_slice_of_the_batch(dev, O, T, N, begin, count):
+    """drcvar_sample_units_f64 draws exactly the whole batch's samples of units [begin, begin+count)
+    (same counters, same arithmetic: bit-equal), including the noise-free step 0 of obstacles whose
+    start falls inside the range — the per-rank sampling of a sharded global batch."""
+    import torch
+    nom = _nominal(dev, O, T)
+    whole = ob.sample_trajectories_device(nom, N, seed=99, stream_offset=5)
+    part = ob.sample_units_device(nom, N, begin, count, seed=99, stream_offset=5)
+    assert part.shape == (count, N, 2)
+    assert torch.equal(part, whole.reshape(O * T, N, 2)[begin:begin + count])
+    # a strided destination (every other unit of a larger buffer)
+    big = torch.full((2 * count + 1, N, 2), -7.0, dtype=torch.float64, device=dev)
+    ob.sample_units_device(nom, N, begin, count, seed=99, stream_offset=5, out=big[::2][:count])
+    assert torch.equal(big[::2][:count], part)
+    if count:
+        assert bool((big[1::2] == -7.0).all())
+
+
+def test_device_sampler_unit_range_validation():
+    import torch
+    if not torch.cuda.is_available():
+        with pytest.raises(ValueError):
+            ob.sample_units_device(torch.zeros((2, 3, 2), dtype=torch.float64), 10, 0, 6)
+        return
+    nom = torch.zeros((2, 3, 2), dtype=torch.float64, device="cuda")
+    with pytest.raises(ValueError):
+        ob.sample_units_device(nom, 10, 4, 3)
