@@ -8,19 +8,23 @@
 A step = one evaluation of the hot path over one batch: every (obstacle, horizon-step) unit of a
 synthetic [O, T, N, 2] fp64 sample tensor -> mean / CVaR / DR-CVaR halfspaces, i.e. ONE launch
 of the fused kernel through the C ABI.  Default workload c3 = BASELINE.json's metric config
-(10 obstacles, T = 20, N = 1000).  Inputs are generated on the device and resident in HBM before
-timing starts.  A c3 launch is ~6 us, so by default the K steps are issued as replays of a
-hipGraph that holds `--graph-batch` consecutive launches (every replayed launch recomputes the
-whole batch; `--launch eager` issues one ctypes call per step instead).
+(10 obstacles, T = 20, N = 1000).  Inputs are drawn on the device and resident in HBM before
+timing starts.  Exactly K steps are timed: by default as replays of a hipGraph of
+G = min(--graph-batch, K) steps plus one graph of the remainder (`--launch eager`: one ctypes
+call per step).
 
-Multi-GPU: one process per GPU; every rank evaluates its own batch (weak scaling, no data-path
-collective); with --gather each step also all-gathers the [U, 8] records over RCCL (the QP
-hand-off exchange).
+Multi-GPU (one process per GPU, RCCL): the global batch has O*N_gpus obstacles; rank r draws
+only its own C3-sized block (units [r*O*T, (r+1)*O*T)) with the device sampler, and a step is
+its launch + an all_gather_into_tensor of the 64-B records to every rank (the exchange the QP
+hand-off needs, core/mpc_filter.py:116-151) -- weak scaling, identical per-GPU work at every N.
+The north-star strong-scaling form is the `strong_scaling` key, at every N: ONE global C5 batch
+(256 x 50 x 10 000) sharded over the ranks + the all-gather, and the full loop with the QP.
 
 Prints ONE JSON line on rank 0: value = units of all ranks / max rank time, plus
-  roofline        the kernel on this workload: algorithmic bytes per launch / (HIP-event time over
-                  the timed region / K) — includes the ~1 us inter-launch gap, so a lower bound
-  roofline_large  the same kernel on a 2 GB resident batch (256 x 50 x 10 000), event-timed
+  roofline        the kernel on this workload: algorithmic bytes per launch / average launch time
+                  (N=1: HIP events over the timed region / K, launch gaps included)
+  strong_scaling  C5 global batch sharded over N ranks (+ all-gather), value and full MPC loop
+  roofline_large  (N=1) the kernel on the resident 2 GB C5 batch, graph-replayed, event-timed
   cpu_baseline    oracle/drcvar_oracle.c (1 thread) on whole batches of the same workload
   max_abs_err     max |offset - oracle| over the benchmarked batch (the metric's second half)
 """
@@ -38,7 +42,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import engine, synthetic  # noqa: E402
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import engine, sharding, synthetic  # noqa: E402
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.engine import RiskParams  # noqa: E402
 
 WORKLOADS = {
@@ -48,14 +52,11 @@ WORKLOADS = {
     "c4": (64, 30, 5000, "synthetic 64 obstacles, T=30, N=5000 (BASELINE config 4, per GPU)"),
     "c5": (256, 50, 10000, "synthetic 256 obstacles, T=50, N=10000 (BASELINE config 5, per GPU)"),
 }
-LARGE = (256, 50, 10000)
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 OUT_BYTES = 64     # 8 fp64 per unit
-
-
-def algorithmic_bytes(O, T, N):
-    """Bytes one launch must move: every sample once (16 B), the 64-B record, ego per step."""
-    return O * T * (16 * N + OUT_BYTES) + T * 16
+# what bounds the sampler (profiles/r02/pmc_sampler*.csv): its per-sample fp64/integer VALU work,
+# not the 16-B store -- its "frac" is the HBM-write fraction it reaches all the same
+SAMPLER_BOUND = "valu"
 
 
 def load_traffic(workload):
@@ -125,35 +126,99 @@ def cpu_baseline(samples, ego, params, budget_s):
 
 
 class Stepper:
-    """Issues steps: eager ctypes launches, or replays of a hipGraph holding G launches."""
+    """Issues exactly the requested number of steps of a `ShardedBatch` (kernel, plus the RCCL
+    all-gather when world > 1): eager ctypes launches, or hipGraph replays — a graph of
+    G = min(graph_batch, steps) steps replayed steps // G times plus a graph of the remainder, so
+    the steps issued are the steps asked for."""
 
-    def __init__(self, samples, ego, params, mode, graph_batch, dev):
-        self.mode = mode
-        self.G = graph_batch if mode == "graph" else 1
-        self.launch, self.out = engine.prepare_safe_halfspaces(samples, ego, params)
+    def __init__(self, sb, mode, graph_batch, steps, dev, exchange=True):
+        self.sb, self.mode, self.dev, self.exchange = sb, mode, dev, exchange
+        self.G = max(1, min(graph_batch, steps)) if mode == "graph" else 1
+        self.rem = steps % self.G if mode == "graph" else 0
+        self.graphs, self._keep = {}, []
         if mode == "graph":
-            self.launch()  # warm the code object before capture
+            self._one()                       # warm the code objects (and the communicator)
             torch.cuda.synchronize(dev)
-            self.graph = torch.cuda.CUDAGraph()
-            cap_stream = torch.cuda.Stream(dev)
-            with torch.cuda.graph(self.graph, stream=cap_stream):
-                # the frozen call must target the capturing stream
-                cap, _ = engine.prepare_safe_halfspaces(samples, ego, params, out=self.out,
-                                                        stream=torch.cuda.current_stream(dev))
-                for _ in range(self.G):
-                    cap()
-            self._keep = cap
+            for n in {self.G, self.rem} - {0}:
+                self.graphs[n] = self._capture(n)
+
+    def _one(self, launch=None):
+        self.sb.compute(launch)
+        if self.exchange:
+            self.sb.exchange()
+
+    def _capture(self, n):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=torch.cuda.Stream(self.dev)):
+            launch = self.sb.prepare(torch.cuda.current_stream(self.dev))  # bound to the capture stream
+            for _ in range(n):
+                self._one(launch)
+        self._keep.append(launch)
+        g.replay()                            # upload the executable graph outside any timed region
+        return g
 
     def run(self, steps):
-        """Issue `steps` steps (rounded up to whole graph replays); returns steps issued."""
+        """Issue exactly `steps` steps; returns the count."""
         if self.mode == "graph":
-            reps = -(-steps // self.G)
-            for _ in range(reps):
-                self.graph.replay()
-            return reps * self.G
+            for _ in range(steps // self.G):
+                self.graphs[self.G].replay()
+            r = steps % self.G
+            if r and r in self.graphs:
+                self.graphs[r].replay()
+            else:                             # (warmup counts other than the timed one)
+                for _ in range(r):
+                    self._one()
+            return steps
         for _ in range(steps):
-            self.launch()
+            self._one()
         return steps
+
+    def describe(self):
+        what = "launch" + (" + RCCL all_gather_into_tensor" if self.exchange and self.sb.full is not None else "")
+        if self.mode == "graph":
+            return (f"hipGraph replays of {self.G} steps (+ one of {self.rem})" if self.rem
+                    else f"hipGraph replays of {self.G} steps") + f"; step = {what}"
+        return f"eager; step = {what}"
+
+
+def timed(world, fn, dev, stream):
+    """The contract's timed region: barrier + synchronize on both sides; returns (wall s, event s
+    on the launching stream, fn's result), each the max over ranks."""
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    res = fn()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    ev_s = ev0.elapsed_time(ev1) * 1e-3
+    if world > 1:
+        red = torch.tensor([elapsed, ev_s], dtype=torch.float64,
+                           device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        elapsed, ev_s = float(red[0]), float(red[1])
+    return elapsed, ev_s, res
+
+
+def kernel_only_time(sb, dev, stream, launches=400, graph_batch=50):
+    """Average duration of this rank's halfspace launch alone: HIP events around graph replays of
+    back-to-back launches (the form the rocprof kernel trace averages)."""
+    st = Stepper(sb, "graph", graph_batch, launches, dev, exchange=False)
+    st.run(launches)                          # warm
+    torch.cuda.synchronize(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    st.run(launches)
+    b.record(stream)
+    torch.cuda.synchronize(dev)
+    return a.elapsed_time(b) * 1e-3 / launches
 
 
 def main():
@@ -164,17 +229,20 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"])
     ap.add_argument("--graph-batch", type=int, default=50)
-    ap.add_argument("--gather", action="store_true", help="all-gather records each step (RCCL)")
+    ap.add_argument("--strong-workload", default="c5", choices=sorted(WORKLOADS),
+                    help="global batch of the strong-scaling line (sharded over the ranks)")
+    ap.add_argument("--strong-steps", type=int, default=20)
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-large", action="store_true", help="skip the 2 GB roofline measurement")
+    ap.add_argument("--no-large", action="store_true",
+                    help="skip everything on the large batch (strong scaling, roofline_large, MPC, sampler)")
     ap.add_argument("--no-mpc", action="store_true", help="skip the MPC hand-off measurement")
-    ap.add_argument("--full-loop", action="store_true",
-                    help="BASELINE config 5's full MPC loop: the GLOBAL batch sharded over ranks, "
-                         "records all-gathered, the DR-CVaR QP solved on every rank (strong scaling)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path (several ranks may share one GPU)")
     args = ap.parse_args()
+    if args.steps < 1:
+        raise SystemExit("--steps must be >= 1")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -191,83 +259,33 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
-
-    if args.full_loop:
-        return full_loop(args, world, rank, dev)
-    O, T, N, desc = WORKLOADS[args.workload]
-    params = RiskParams()  # config/parameters.py: alpha 0.2, delta 0.1, eps 0.15, radii 0.3/0.3
-    samples, ego = synthetic.obstacle_batch(O, T, N, dev, seed=42 + rank)
-    U = O * T
-    mode = "eager" if (args.gather and world > 1) else args.launch  # collectives stay eager
-    stepper = Stepper(samples, ego, params, mode, args.graph_batch, dev)
-    out = stepper.out
-    gathered = None
-    if args.gather and world > 1:
-        gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-        gathered = torch.empty((U * world, engine.OUT_WIDTH), dtype=torch.float64, device=gdev)
-
-    def steps(k):
-        if gathered is None:
-            return stepper.run(k)
-        for _ in range(k):
-            stepper.launch()
-            rec = out.view(U, engine.OUT_WIDTH)
-            dist.all_gather_into_tensor(gathered, rec if gathered.is_cuda else rec.cpu())
-        return k
-
-    steps(args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-
+    gdev = "cpu" if (world > 1 and args.dist_backend == "gloo") else None
+    mode = "eager" if (world > 1 and args.dist_backend == "gloo") else args.launch
     stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    K = steps(args.steps)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kernel_s = ev0.elapsed_time(ev1) * 1e-3 / K
+    params = RiskParams()  # config/parameters.py: alpha 0.2, delta 0.1, eps 0.15, radii 0.3/0.3
 
-    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    t_max = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    elapsed, kernel_s = float(t_max[0].item()), float(t_max[1].item())
+    # ---- the metric line: every rank's shard is exactly the workload (weak scaling) ----
+    O, T, N, desc = WORKLOADS[args.workload]
+    nominal = synthetic.nominal_paths(O * world, T, dev, seed=42)   # the global (O*world)-obstacle batch
+    ego = synthetic.straight_line_ego(T, dev)
+    sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=42, gather_device=gdev)
+    assert sb.count == O * T
+    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev)
+    stepper.run(args.warmup)                   # untimed warmup (W steps)
+    elapsed, ev_s, K = timed(world, lambda: stepper.run(args.steps), dev, stream)
+    if world == 1:
+        kernel_s, ktiming = ev_s / K, "HIP events over the timed region / K (launch gaps included)"
+    else:
+        kernel_s = kernel_only_time(sb, dev, stream, graph_batch=args.graph_batch)
+        ktiming = "HIP events over graph-replayed kernel-only launches (the timed steps also carry the all-gather)"
 
-    large = mpc = sampling = None
-    if rank == 0 and not args.no_large:
-        Ol, Tl, Nl = LARGE
-        s_l, e_l = synthetic.obstacle_batch(Ol, Tl, Nl, dev, seed=7)
-        launch_l, _ = engine.prepare_safe_halfspaces(s_l, e_l, params)
-        for _ in range(3):
-            launch_l()
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 20
-        a.record(stream)
-        for _ in range(reps):
-            launch_l()
-        b.record(stream)
-        torch.cuda.synchronize()
-        large = roofline(algorithmic_bytes(Ol, Tl, Nl), a.elapsed_time(b) * 1e-3 / reps,
-                         load_traffic("c5"))
-        large["workload"] = f"{Ol} obstacles x {Tl} steps x {Nl} samples (2.05 GB resident)"
-        large["halfspaces_per_s"] = Ol * Tl / (large["kernel_ms"] * 1e-3)
-        sampling = sampler_roofline(s_l, stream)
-        if not args.no_mpc:
-            mpc = mpc_handoff(dev, s_l, e_l, params, with_cpu=world == 1 and not args.no_cpu_baseline)
-        del s_l, e_l
-        torch.cuda.empty_cache()
+    strong = None
+    if not args.no_large and not args.no_strong:
+        strong = strong_scaling(args, world, rank, dev, stream, params, gdev, mode)
 
     result = None
     if rank == 0:
-        value = U * world * K / elapsed
+        value = sb.U * K / elapsed               # units of ALL ranks (sb.U = O * world * T)
         result = {
             "metric": "halfspace-constraints/sec (N=1000, 10 obs, T=20) + max |offset - ref|",
             "value": value,
@@ -282,20 +300,38 @@ def main():
             "dtype": "f64",
             "data": "synthetic (device-generated obstacle samples, SURVEY.md §8d distributions)",
             "config": {"workload": f"{args.workload}: {desc}", "obstacles": O, "steps": T,
-                       "samples": N, "units_per_gpu": U, "global_units_per_step": U * world,
-                       "parallelism": f"dp{world}" + ("+allgather" if gathered is not None else ""),
-                       "launch": (f"hipGraph replays of {stepper.G} launches" if mode == "graph"
-                                  else "eager ctypes launch per step"),
+                       "samples": N, "units_per_gpu": sb.count, "global_units_per_step": sb.U,
+                       "global_batch": f"{O * world} obstacles x {T} steps x {N} samples, obstacles "
+                                       f"[{O}r, {O}r + {O}) on rank r",
+                       "parallelism": f"dp{world}" + ("+allgather" if world > 1 else ""),
+                       "launch": stepper.describe(),
                        "alpha": params.alpha, "delta": params.delta, "epsilon": params.epsilon},
-            "roofline": roofline(algorithmic_bytes(O, T, N), kernel_s, load_traffic(args.workload)),
-            "roofline_large": large,
-            "mpc_handoff": mpc,
-            "sampling": sampling,
+            "roofline": dict(roofline(sb.algorithmic_bytes, kernel_s, load_traffic(args.workload)),
+                             timing=ktiming),
+            "strong_scaling": strong,
         }
+    large = mpc = sampling = None
+    if rank == 0 and world == 1 and not args.no_large and strong is not None:
+        big = strong.pop("_batch")
+        large = strong.pop("_roofline")
+        sampling = sampler_roofline(big, stream)
+        if not args.no_mpc:
+            mpc = mpc_handoff(dev, big.samples.view(big.O, big.T, big.N, 2), big.ego_units[:big.T],
+                              params, with_cpu=not args.no_cpu_baseline)
+        del big
+        torch.cuda.empty_cache()
+    elif strong is not None:
+        strong.pop("_batch", None)
+        strong.pop("_roofline", None)
+    if rank == 0:
+        result["roofline_large"] = large
+        result["mpc_handoff"] = mpc
+        result["sampling"] = sampling
         if world == 1 and not args.no_cpu_baseline:
             import numpy as np
-            ref, base = cpu_baseline(samples, ego, params, args.cpu_seconds)
-            got = out.cpu().numpy()
+            samples4 = sb.samples.view(O, T, N, 2)
+            ref, base = cpu_baseline(samples4, ego, params, args.cpu_seconds)
+            got = sb.records().cpu().numpy()
             result["max_abs_err"] = float(np.max(np.abs(got[..., [2, 5, 6, 7]] - ref[..., [2, 5, 6, 7]])))
             result["max_abs_err_h"] = float(np.max(np.abs(got[..., [0, 1, 3, 4]] - ref[..., [0, 1, 3, 4]])))
             base["host_cpu"] = _cpu_model()
@@ -310,102 +346,82 @@ def main():
     return result
 
 
-def full_loop(args, world, rank, dev):
-    """One step = this rank's contiguous block of the global (obstacle x step) units through the
-    halfspace kernel -> all_gather_into_tensor of the 64-B records (RCCL) -> the DR-CVaR safety
-    filter QP over all O*T halfspaces (H = T) on every rank.  value = global units / max rank time.
-    """
-    import numpy as np
-    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import sharding
-    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
-    O, T, N, desc = WORKLOADS[args.workload]
-    params = RiskParams()
-    samples, ego = synthetic.obstacle_batch(O, T, N, dev, seed=42)       # same global batch on all ranks
-    U = O * T
-    s_u, e_u, start, stop = sharding.shard_units(samples, ego, world, rank)
-    local = torch.empty((max(stop - start, 0), engine.OUT_WIDTH), dtype=torch.float64, device=dev)
-    launch = None
-    if stop > start:
-        launch, local = engine.prepare_safe_halfspaces(s_u.unsqueeze(0), e_u, params,
-                                                       out=local.view(1, stop - start, engine.OUT_WIDTH))
-        local = local.view(stop - start, engine.OUT_WIDTH)
-    per = -(-U // world)
-    padded = torch.zeros((per, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
-    gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    full = torch.empty((per * world, engine.OUT_WIDTH), dtype=torch.float64, device=gdev)
-    dt = 0.2
-    A = np.block([[np.eye(2), dt * np.eye(2)], [np.zeros((2, 2)), np.eye(2)]])
-    Bm = np.block([[0.5 * dt ** 2 * np.eye(2)], [dt * np.eye(2)]])
-    C = np.block([np.eye(2), np.zeros((2, 2))])
-    model = mf.MPCModel(A, Bm, C, 2 * np.eye(4), np.eye(2), T, (np.full(2, -5.0), np.full(2, 5.0)),
-                        (np.full(2, -10.0), np.full(2, 10.0)), device=dev)
-    x0, xr, uf, _ = _mpc_problem_inputs(ego, T, 1, dev)
-    ws = torch.empty(model.workspace_doubles(1, O), dtype=torch.float64, device=dev)
-    rec_dev = torch.empty((U, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
-    res = {}
+def strong_scaling(args, world, rank, dev, stream, params, gdev, mode):
+    """The north-star multi-GPU form (BASELINE configs 4/5): ONE global batch (default C5,
+    256 x 50 x 10 000, 2.05 GB) sharded over the ranks — each rank draws only its contiguous unit
+    block on its device, the kernel writes into its slice of the all-gather input and the records
+    are all-gathered over RCCL inside the timed region.  Identical global work at every N (strong
+    scaling); at N = 1 the exchange is the identity and is skipped.  Also times the full MPC loop
+    (shard kernel -> all-gather -> the DR-CVaR QP over all O*T halfspaces, replicated per rank)."""
+    O, T, N, desc = WORKLOADS[args.strong_workload]
+    nominal = synthetic.nominal_paths(O, T, dev, seed=7)
+    ego = synthetic.straight_line_ego(T, dev)
+    sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=7, gather_device=gdev)
+    K = args.strong_steps
+    st = Stepper(sb, mode, 10, K, dev)
+    st.run(min(K, 10))
+    elapsed, _, _ = timed(world, lambda: st.run(K), dev, stream)
+    kernel_s = kernel_only_time(sb, dev, stream, launches=20, graph_batch=10)
+    out = {"workload": f"{args.strong_workload}: {desc}, global batch sharded over {world} rank(s)",
+           "value": sb.U * K / elapsed, "unit": "halfspace-constraints/s", "n_gpus": world,
+           "steps": K, "ms_per_step": elapsed / K * 1e3, "scaling": "strong",
+           "units_global": sb.U, "units_per_rank": sb.per,
+           "parallelism": f"dp{world}" + ("+allgather (RCCL)" if world > 1 else ""),
+           "launch": st.describe(),
+           "rank0_kernel_ms": kernel_s * 1e3,
+           "rank0_kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK}
+    del st
+    # full loop: + the QP hand-off on every rank (core/mpc_filter.py:116-151 takes all halfspaces)
+    if not args.no_mpc:
+        import numpy as np
+        from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+        dt = 0.2
+        A = np.block([[np.eye(2), dt * np.eye(2)], [np.zeros((2, 2)), np.eye(2)]])
+        Bm = np.block([[0.5 * dt ** 2 * np.eye(2)], [dt * np.eye(2)]])
+        C = np.block([np.eye(2), np.zeros((2, 2))])
+        model = mf.MPCModel(A, Bm, C, 2 * np.eye(4), np.eye(2), T, (np.full(2, -5.0), np.full(2, 5.0)),
+                            (np.full(2, -10.0), np.full(2, 10.0)), device=dev)
+        x0, xr, uf, _ = _mpc_problem_inputs(ego, T, 1, dev)
+        ws = torch.empty(model.workspace_doubles(1, O), dtype=torch.float64, device=dev)
+        rec = sb.records()
+        if rec.device != dev:
+            rec = torch.empty(rec.shape, dtype=torch.float64, device=dev)
+        h, g = mf.record_views(rec, "dr_cvar")
+        res = {}
 
-    def step():
-        if launch is not None:
-            launch()
-        if world > 1:
-            padded[: stop - start] = local
-            dist.all_gather_into_tensor(full, padded if full.is_cuda else padded.cpu())
-            rec_dev.copy_(full[:U], non_blocking=True)
-            rec = rec_dev
-        else:
-            rec = local
-        h, g = mf.record_views(rec.view(O, T, engine.OUT_WIDTH), "dr_cvar")
-        res["u"], res["info"] = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws)[1:]
+        def loop(k):
+            for _ in range(k):
+                sb.step()
+                if sb.full is not None and sb.full.device != dev:
+                    rec.copy_(sb.records())
+                res["info"] = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws)[2]
+            return k
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    elapsed = float(t_max[0].item())
-    result = None
-    if rank == 0:
+        Kf = 5
+        loop(2)
+        el, _, _ = timed(world, lambda: loop(Kf), dev, stream)
         info = res["info"][0].cpu().numpy()
-        result = {
-            "metric": "full MPC loop halfspace-constraints/sec (BASELINE config 5: halfspaces + "
-                      "all-gather + QP hand-off)",
-            "value": U * args.steps / elapsed, "unit": "halfspace-constraints/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (device-sampled obstacle batch, identical on every rank)",
-            "config": {"workload": f"{args.workload}: {desc}", "units": U,
-                       "parallelism": f"units sharded dp{world} + allgather + replicated QP",
-                       "qp": f"dr_cvar safety filter, H={T}, {U} halfspace rows"},
-            "qp_status": int(info[0]), "qp_iterations": int(info[1]),
-            "roofline": None, "cpu_baseline": None,
-        }
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return result
+        out["full_loop"] = {"steps": Kf, "ms_per_step": el / Kf * 1e3,
+                            "halfspace_constraints_per_s": sb.U * Kf / el,
+                            "qp": f"dr_cvar safety filter, H={T}, {sb.U} halfspace rows, one problem, "
+                                  f"replicated on every rank",
+                            "qp_status": mf.STATUS_NAMES.get(int(info[0])), "qp_iterations": int(info[1])}
+    if rank == 0 and world == 1:
+        out["_batch"] = sb
+        large = roofline(sb.algorithmic_bytes, kernel_s, load_traffic("c5"))
+        large["workload"] = f"{O} obstacles x {T} steps x {N} samples (2.05 GB resident)"
+        large["halfspaces_per_s"] = sb.U / kernel_s
+        large["timing"] = "HIP events over 20 graph-replayed launches (2 replays of 10)"
+        out["_roofline"] = large
+    return out
 
 
-def sampler_roofline(out, stream, reps=10):
-    """Device sample generator (drcvar_sample_trajectories_f64) refilling a resident batch: bytes
-    written (16 per sample) per launch / event time -- an HBM-write-bound kernel."""
+def sampler_roofline(sb, stream, reps=10):
+    """Device sample generator (drcvar_sample_units_f64) refilling the resident large batch with
+    the same draws: bytes written (16 per sample) per launch / event time."""
     from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.simulation import obstacles
-    O, T, N, _ = out.shape
-    nominal = out[:, :, 0, :].clone()                    # any [O, T, 2] nominal path
-    launch = lambda: obstacles.sample_trajectories_device(nominal, N, seed=11, out=out)
+    launch = lambda: obstacles.sample_units_device(sb.nominal, sb.N, sb.start, sb.count, seed=sb.seed,
+                                                   out=sb.samples)
     launch()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -415,10 +431,12 @@ def sampler_roofline(out, stream, reps=10):
     b.record(stream)
     torch.cuda.synchronize()
     sec = a.elapsed_time(b) * 1e-3 / reps
-    written = O * T * N * 16
-    return {"workload": f"{O}x{T}x{N} samples (Philox4x32-10 + Box-Muller, fp64)", "kernel_ms": sec * 1e3,
-            "samples_per_s": O * T * N / sec, "bound": "hbm", "achieved": written / sec / 1e9,
-            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": written / sec / HBM_PEAK}
+    n = sb.count * sb.N
+    written = n * 16
+    return {"workload": f"{sb.count} units x {sb.N} samples (Philox4x32-10 + Box-Muller, fp64)",
+            "kernel_ms": sec * 1e3, "samples_per_s": n / sec, "bound": SAMPLER_BOUND,
+            "achieved": written / sec / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": written / sec / HBM_PEAK}
 
 
 def _mpc_problem_inputs(ego, H, B, dev):

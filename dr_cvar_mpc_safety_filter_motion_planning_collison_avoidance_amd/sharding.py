@@ -86,10 +86,8 @@ def engine_compute(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams,
 def _all_gather(full: torch.Tensor, send: torch.Tensor, group=None) -> None:
     if full.device == send.device:
         dist.all_gather_into_tensor(full, send, group=group)
-    else:                                           # gloo rehearsal of device records
-        host = torch.empty_like(full, device=full.device)
-        dist.all_gather_into_tensor(host, send.to(full.device), group=group)
-        full.copy_(host)
+    else:                                           # gloo rehearsal: device records via the host
+        dist.all_gather_into_tensor(full, send.to(full.device), group=group)
 
 
 def gather_records(send: torch.Tensor, n_units: int, group=None) -> torch.Tensor:
@@ -140,7 +138,7 @@ class ShardedBatch:
         self.O, self.T, self.N = O, T, int(n_samples)
         self.U = O * T
         self.world, self.rank, self.group = world_size, rank, group
-        self.params = params
+        self.params, self.nominal, self.seed = params, nominal, seed
         self.start, self.stop = shard_bounds(self.U, world_size, rank)
         self.count = self.stop - self.start
         self.per = -(-self.U // world_size) if self.U else 0
