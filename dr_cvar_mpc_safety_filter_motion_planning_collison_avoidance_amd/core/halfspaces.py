@@ -149,11 +149,45 @@ class HalfspaceBatch:
         return out
 
 
+def launch_with_singletons(launch, keys, shape, robot_radius, obstacle_radius):
+    """Records of a grid of units whose CVaR / DR-CVaR parameters come from the reference's
+    N-keyed optimiser singletons (``risk_metrics.singleton_params``).
+
+    ``launch(params) -> [*shape, 8]`` evaluates the whole grid with one parameter set; ``keys``
+    lists ``((a_c, d_c), (a_d, d_d, e_d))`` per unit in row-major order of ``shape``.  Every
+    column but ``g_cvar`` comes from the unit's DR-CVaR parameters (the directions and the mean
+    halfspace do not depend on them), ``g_cvar`` from its CVaR parameters.  The usual case — one
+    parameter set for the whole grid, CVaR equal to DR — is ONE launch; each further distinct
+    set costs one more launch of the grid.
+    """
+    def pset(a, d, e):
+        return RiskParams(robot_radius, obstacle_radius, a, d, e)
+    dr_of = [pset(*dk) for _, dk in keys]
+    cv_of = [dr if ck == dk[:2] else pset(ck[0], ck[1], dk[2]) for (ck, dk), dr in zip(keys, dr_of)]
+    needed = list(dict.fromkeys(dr_of + cv_of))
+    recs = {p: launch(p) for p in needed}
+    first = recs[needed[0]]
+    if len(needed) == 1:
+        return first
+    out = torch.empty_like(first)
+    flat = out.view(-1, engine.OUT_WIDTH)
+    for p, r in recs.items():                     # whole rows from the DR-CVaR parameters ...
+        m_dr = torch.as_tensor([q == p for q in dr_of], device=out.device)
+        flat[m_dr] = r.reshape(-1, engine.OUT_WIDTH)[m_dr]
+    col = flat[:, _native.COL_G_CVAR]
+    for p, r in recs.items():                     # ... then g_cvar from the CVaR parameters
+        m_cv = torch.as_tensor([q == p for q in cv_of], device=out.device)
+        col[m_cv] = r.reshape(-1, engine.OUT_WIDTH)[m_cv, _native.COL_G_CVAR]
+    return out
+
+
 def compute_safe_halfspaces_batched(samples, ego, robot_radius, obstacle_radius, alpha, delta,
                                     epsilon, stream=None) -> HalfspaceBatch:
     """Every (obstacle, step) unit of ``samples`` [O, T, N, 2] against ``ego`` [T, 2] in one launch.
 
-    Accepts device tensors (no copy) or host arrays (staged to the current HIP device).
+    Accepts device tensors (no copy) or host arrays (staged to the current HIP device).  A build
+    API (the reference has no batched call): the parameters given are the parameters used — the
+    optimiser singletons are neither read nor changed.
     """
     params = RiskParams(robot_radius, obstacle_radius, alpha, delta, epsilon)
     t0 = time.time()
@@ -172,10 +206,14 @@ def compute_safe_halfspaces(obstacle_samples, ego_ref_pos, robot_radius, obstacl
     """Safe halfspaces for a list of per-obstacle sample arrays ``[N_i, 2]`` (:196-248).
 
     Returns ``{'mean': [...], 'cvar': [...], 'dr_cvar': [...]}`` with one SafeHalfspace per
-    obstacle, in input order.  Obstacles with equal N share one kernel launch.
+    obstacle, in input order.  Obstacles with equal N share one kernel launch.  Like the
+    reference (which reaches its LPs through ``cvar_halfspace`` / ``dr_cvar_halfspace``), each
+    obstacle is solved with the parameters of the optimiser singleton for its N
+    (``risk_metrics.singleton_params``), and the singletons are left as the reference leaves them.
+    ``.info`` of every CVaR / DR-CVaR object is this call's staging / kernel time divided evenly
+    over the obstacles (the reference's is the JSON of that obstacle's own last LP solve).
     """
-    params = RiskParams(robot_radius, obstacle_radius, alpha, delta, epsilon)
-    params.validate()
+    RiskParams(robot_radius, obstacle_radius, alpha, delta, epsilon).validate()
     n_obstacles = len(obstacle_samples)
     result = {"mean": [None] * n_obstacles, "cvar": [None] * n_obstacles,
               "dr_cvar": [None] * n_obstacles}
@@ -183,16 +221,21 @@ def compute_safe_halfspaces(obstacle_samples, ego_ref_pos, robot_radius, obstacl
         return {"mean": [], "cvar": [], "dr_cvar": []}
     t0 = time.time()
     dev = risk_metrics.device()
+    counts = [int(np.shape(s)[0]) for s in obstacle_samples]
+    keys = risk_metrics.singleton_params(counts, alpha, delta, epsilon)
     groups: dict[int, list[int]] = {}
-    for i, s in enumerate(obstacle_samples):
-        groups.setdefault(int(np.shape(s)[0]), []).append(i)
+    for i, n in enumerate(counts):
+        groups.setdefault(n, []).append(i)
     ego = torch.as_tensor(np.asarray(ego_ref_pos, dtype=np.float64).reshape(1, 2)).to(dev)
     staged = []
     for n, idx in groups.items():
         host = np.stack([np.asarray(obstacle_samples[i], dtype=np.float64) for i in idx])
         staged.append((idx, torch.as_tensor(host).to(dev).reshape(len(idx), 1, n, 2)))
     t1 = time.time()
-    recs = [(idx, engine.safe_halfspaces(s, ego, params)) for idx, s in staged]
+    recs = [(idx, launch_with_singletons(lambda p, s=s: engine.safe_halfspaces(s, ego, p),
+                                         [keys[i] for i in idx], (len(idx), 1),
+                                         robot_radius, obstacle_radius))
+            for idx, s in staged]
     host_recs = [(idx, r.cpu().numpy()) for idx, r in recs]
     t2 = time.time()
     per = {"setup_time": (t1 - t0) / n_obstacles, "solve_time": (t2 - t1) / n_obstacles}

@@ -9,7 +9,9 @@ contract, but there is no LP to build: the GPU kernel evaluates the LP optimum i
 
 * module-level optimiser singletons keyed on ``n_samples`` only (:12-13, :289, :325) — like the
   reference, ``dr_cvar_halfspace`` / ``cvar_halfspace`` keep the alpha/delta/epsilon of the first
-  call for a given N (call :func:`reset_optimizers` to drop them);
+  call for a given N, and so do the batched ``compute_safe_halfspaces`` and
+  ``SafetyFilteringEnvironment`` paths (:func:`singleton_params`); call :func:`reset_optimizers`
+  to drop them;
 * ``tmp/timing_info_{drcvar,cvar}.json`` side channel with ``setup_time`` / ``solve_time`` seconds
   (:16-33), which ``core/halfspaces.py`` and ``evaluation/timing_analysis.py`` read back;
 * solver-failure sentinels (:173-177, :261-265, :298-303, :334-338): ``g = 100.0`` and
@@ -150,6 +152,31 @@ def cvar_halfspace(samples, h, alpha, delta, robot_radius, obstacle_radius):
     combined_radius = robot_radius + obstacle_radius
     solved, g_value, _ = cvar_optimizer.solve(h, samples, combined_radius)
     return g_value if solved else 100.0
+
+
+def singleton_params(sample_counts, alpha, delta, epsilon):
+    """The parameters the reference's optimiser singletons solve each call with.
+
+    The reference reaches its LPs only through ``cvar_halfspace`` / ``dr_cvar_halfspace``, whose
+    module singletons are keyed on N alone (:289, :325): a call whose N matches the live singleton
+    keeps the alpha/delta(/epsilon) the singleton was built with, any other N rebuilds it with the
+    call's values — CVaR and DR-CVaR independently.  ``sample_counts`` lists N for every solve in
+    the reference's call order (per ``compute_safe_halfspaces`` call: obstacles in order; per
+    ``compute_safe_halfspaces_for_trajectory``: steps outer, obstacles inner).  The singletons are
+    updated exactly as those calls would leave them.  Returns per call
+    ``((alpha_cvar, delta_cvar), (alpha_dr, delta_dr, epsilon_dr))``.
+    """
+    global drcvar_optimizer, cvar_optimizer
+    keys = []
+    for n in sample_counts:
+        n = int(n)
+        if drcvar_optimizer is None or drcvar_optimizer.n_samples != n:
+            drcvar_optimizer = DRCVaROptimizer(alpha, epsilon, delta, n)
+        if cvar_optimizer is None or cvar_optimizer.n_samples != n:
+            cvar_optimizer = CVaROptimizer(alpha, delta, n)
+        keys.append(((cvar_optimizer.alpha, cvar_optimizer.delta),
+                     (drcvar_optimizer.alpha, drcvar_optimizer.delta, drcvar_optimizer.epsilon)))
+    return keys
 
 
 def reset_optimizers() -> None:

@@ -17,6 +17,7 @@ import torch
 
 from .. import engine
 from ..core import risk_metrics
+from ..core import halfspaces as hs_mod
 from ..core.halfspaces import HalfspaceBatch
 from ..engine import RiskParams
 
@@ -55,11 +56,16 @@ class SafetyFilteringEnvironment:
         self.input_bounds = input_bounds
 
     def compute_halfspace_batch(self, obstacle_sample_trajectories, ego_ref_trajectory):
-        """Device-side result: a HalfspaceBatch whose record is [O, T, 8] (T = min(len(ref), H))."""
+        """Device-side result: a HalfspaceBatch whose record is [O, T, 8] (T = min(len(ref), H)).
+
+        Each unit is solved with the parameters of the reference's optimiser singleton for its N
+        (``risk_metrics.singleton_params`` over the reference's call order: steps outer,
+        obstacles inner), so a previous call with the same N but other alpha/delta/epsilon
+        carries over exactly as in the reference; usually that is one launch per distinct N.
+        """
         n_obstacles = len(obstacle_sample_trajectories)
         n_steps = min(len(ego_ref_trajectory), self.HORIZON)               # environment.py:72
-        params = self.params
-        params.validate()
+        self.params.validate()
         t0 = time.time()
         dev = risk_metrics.device()
         ego = np.asarray(ego_ref_trajectory, dtype=np.float64)[:n_steps] @ self.C.T  # :92
@@ -68,27 +74,53 @@ class SafetyFilteringEnvironment:
                              device=dev)
         if n_obstacles == 0 or n_steps == 0:
             return HalfspaceBatch(record)
+        counts = [int(np.shape(tr)[0]) for tr in obstacle_sample_trajectories]
+        keys = risk_metrics.singleton_params([counts[o] for _ in range(n_steps)
+                                              for o in range(n_obstacles)],
+                                             self.ALPHA, self.DELTA, self.EPSILON)
         groups: dict[int, list[int]] = {}
-        for i, tr in enumerate(obstacle_sample_trajectories):
-            groups.setdefault(int(np.shape(tr)[0]), []).append(i)
+        for i, n in enumerate(counts):
+            groups.setdefault(n, []).append(i)
         launches = []
         for n, idx in groups.items():
             # [G, N, n_steps, 2] slice of the reference layout, staged as-is (environment.py:88)
             host = np.stack([np.asarray(obstacle_sample_trajectories[i], dtype=np.float64)[:, :n_steps, :]
                              for i in idx])
-            # one pinned staging copy, asynchronous H2D; the kernel reads the reference's
-            # [G, N, T, 2] order through strides (no transpose pass)
-            dev_s = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
+            # one pinned staging buffer (cached, grown on demand), asynchronous H2D; the kernel
+            # reads the reference's [G, N, T, 2] order through strides (no transpose pass)
+            stage = self._pinned_stage(host.size).view(-1)[:host.size].view(host.shape)
+            stage.copy_(torch.from_numpy(host))
+            dev_s = stage.to(dev, non_blocking=True)
+            self._stage_event = torch.cuda.Event()
+            self._stage_event.record()
             view = dev_s.permute(0, 2, 1, 3)                                  # [G, T, N, 2] strided
-            launches.append((idx, view))
+            # unit (g, t) is call t * O + o of the reference's loop
+            gkeys = [keys[t * n_obstacles + o] for o in idx for t in range(n_steps)]
+            launches.append((idx, view, gkeys))
         t1 = time.time()
-        for idx, view in launches:
-            out = engine.safe_halfspaces(view, ego_d, params)
+        params = self.params
+        for idx, view, gkeys in launches:
+            out = hs_mod.launch_with_singletons(
+                lambda p, v=view: engine.safe_halfspaces(v, ego_d, p), gkeys,
+                (len(idx), n_steps), params.robot_radius, params.obstacle_radius)
             if len(idx) == n_obstacles:
                 record = out
             else:
                 record[torch.as_tensor(idx, device=dev)] = out
         return HalfspaceBatch(record, setup_time=t1 - t0)
+
+    def _pinned_stage(self, n_doubles):
+        """The cached pinned host buffer the trajectories are staged through (one allocation for
+        the environment's lifetime unless a larger batch arrives).  Before it is refilled, the
+        previous asynchronous copy out of it must have finished."""
+        ev = getattr(self, "_stage_event", None)
+        if ev is not None:
+            ev.synchronize()
+        buf = getattr(self, "_stage_buf", None)
+        if buf is None or buf.numel() < n_doubles:
+            buf = torch.empty(int(n_doubles), dtype=torch.float64).pin_memory()
+            self._stage_buf = buf
+        return buf
 
     def compute_safe_halfspaces_for_trajectory(self, obstacle_sample_trajectories,
                                                ego_ref_trajectory):

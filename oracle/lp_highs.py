@@ -37,11 +37,11 @@ def _h_xi(h, samples):
     return samples @ h                                           # risk_metrics.py:145 / :233
 
 
-def solve_cvar_lp(samples, h, alpha, delta, robot_radius, obstacle_radius):
-    """``cvar_halfspace`` (risk_metrics.py:305-338) with the LP of :182-213. Returns g."""
-    hxi = _h_xi(h, samples)
+def cvar_lp(h_xi, r, alpha, delta):
+    """The CVaR LP of :182-213 on its parameters (``h_xi_param`` = h.xi_i, ``r_param``).
+    Returns ``(solved, g)``."""
+    hxi = np.asarray(h_xi, dtype=np.float64).reshape(-1)
     n = hxi.shape[0]
-    r = (robot_radius + obstacle_radius) * np.linalg.norm(h)    # :329 and :234
     nv = 2 + n
     c = np.zeros(nv)
     c[0] = 1.0
@@ -59,15 +59,15 @@ def solve_cvar_lp(samples, h, alpha, delta, robot_radius, obstacle_radius):
     bounds = [(None, None), (None, None)] + [(0.0, None)] * n
     res = linprog(c, A_ub=A, b_ub=b, bounds=bounds, method="highs")
     if res.status != 0:
-        return SENTINEL
-    return float(res.x[0])
+        return False, SENTINEL
+    return True, float(res.x[0])
 
 
-def solve_dr_cvar_lp(samples, h, alpha, delta, epsilon, robot_radius, obstacle_radius):
-    """``dr_cvar_halfspace`` (risk_metrics.py:267-303) with the LP of :87-125. Returns (g*, g~)."""
-    hxi = _h_xi(h, samples)
+def dr_cvar_lp(h_xi, r, alpha, delta, epsilon):
+    """The DR-CVaR LP of :87-125 on its parameters (``h_xi_param``, ``r_param``).
+    Returns ``(solved, g*)``."""
+    hxi = np.asarray(h_xi, dtype=np.float64).reshape(-1)
     n = hxi.shape[0]
-    r = (robot_radius + obstacle_radius) * np.linalg.norm(h)    # :293
     a_k = (-1.0 / alpha, 0.0)
     b_k = (-1.0 / alpha, 0.0)
     c_k = (1.0 - 1.0 / alpha, 1.0)
@@ -94,6 +94,20 @@ def solve_dr_cvar_lp(samples, h, alpha, delta, epsilon, robot_radius, obstacle_r
     bounds = [(None, None), (None, None), (max(0.0, 1.0 / alpha), None)] + [(None, None)] * n
     res = linprog(c, A_ub=A, b_ub=b, bounds=bounds, method="highs")
     if res.status != 0:
+        return False, SENTINEL
+    return True, float(res.x[0])
+
+
+def solve_cvar_lp(samples, h, alpha, delta, robot_radius, obstacle_radius):
+    """``cvar_halfspace`` (risk_metrics.py:305-338) with the LP of :182-213. Returns g."""
+    r = (robot_radius + obstacle_radius) * np.linalg.norm(h)    # :329 and :234
+    return cvar_lp(_h_xi(h, samples), r, alpha, delta)[1]
+
+
+def solve_dr_cvar_lp(samples, h, alpha, delta, epsilon, robot_radius, obstacle_radius):
+    """``dr_cvar_halfspace`` (risk_metrics.py:267-303) with the LP of :87-125. Returns (g*, g~)."""
+    r = (robot_radius + obstacle_radius) * np.linalg.norm(h)    # :293
+    ok, g_star = dr_cvar_lp(_h_xi(h, samples), r, alpha, delta, epsilon)
+    if not ok:
         return SENTINEL, SENTINEL - r
-    g_star = float(res.x[0])
     return g_star, g_star - r
