@@ -17,7 +17,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in ${STEPS:-pytest smoke bench bench_c5 prof mpcprof pmc}; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench_eager) step bench_eager 600 python bench.py --launch eager --no-large --no-cpu-baseline ;;
