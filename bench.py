@@ -506,9 +506,22 @@ def mpc_handoff(dev, samples, ego, params, with_cpu):
     full_ms = timed(full, 5)
     qp_ms = timed(qp, 5)
     info = res["info"][0].cpu().numpy()
+    groups = model.launch_groups(1, O)
+    # the same QP on one workgroup (DRCVAR_MPC_CLUSTER=1), for comparison with the clustered launch
+    prev = os.environ.get("DRCVAR_MPC_CLUSTER")
+    os.environ["DRCVAR_MPC_CLUSTER"] = "1"
+    try:
+        qp1_ms = timed(qp, 3)
+    finally:
+        if prev is None:
+            del os.environ["DRCVAR_MPC_CLUSTER"]
+        else:
+            os.environ["DRCVAR_MPC_CLUSTER"] = prev
+    qp()  # leaves the clustered answer in res
     c5 = {"workload": f"{O} obstacles x {T} steps x {samples.shape[2]} samples -> dr_cvar QP "
                       f"(H={H}, {O * T} halfspace rows), 1 problem",
           "full_step_ms": full_ms, "qp_ms": qp_ms, "halfspace_ms": full_ms - qp_ms,
+          "qp_workgroups": groups, "qp_one_workgroup_ms": qp1_ms,
           "halfspace_constraints_per_s_full_loop": O * T / (full_ms * 1e-3),
           "qp_status": mf.STATUS_NAMES.get(int(info[_native.MPC_INFO_STATUS])),
           "qp_iterations": int(info[_native.MPC_INFO_ITERATIONS]),
@@ -557,9 +570,10 @@ def mpc_handoff(dev, samples, ego, params, with_cpu):
                               "sample": f"{reps} solves of problem 0 by oracle/mpc_qp.py ({el:.1f} s)"}
         br["max_abs_err_u_vs_oracle"] = float(np.abs(res["u"][0].cpu().numpy() - uo).max())
     out["batched_reference"] = br
-    out["bound"] = ("latency: one workgroup per problem runs the whole interior-point solve "
-                    "(Riccati factorisation + solves on one wave, and at C5 the row passes over "
-                    "12 800 halfspaces, dominate; see DESIGN.md)")
+    out["bound"] = ("latency: every interior-point iteration is a chain of Riccati factorisation "
+                    "and solves on one wave; batches run one workgroup per problem, a large problem "
+                    "(C5: 12 800 halfspace rows) a cluster of workgroups that split the row sweeps "
+                    "and exchange row sums in the launch (see DESIGN.md)")
     return out
 
 

@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "drcvar_launch_plan",
     "drcvar_mpc_model_init",
     "drcvar_mpc_workspace_doubles",
+    "drcvar_mpc_launch_groups",
     "drcvar_mpc_filter_f64",
     "drcvar_sample_trajectories_f64",
     "drcvar_sample_units_f64",
@@ -137,6 +138,8 @@ def _bind(lib):
     lib.drcvar_mpc_model_init.restype = ctypes.c_int
     lib.drcvar_mpc_workspace_doubles.argtypes = [modelp, i64, i64]
     lib.drcvar_mpc_workspace_doubles.restype = i64
+    lib.drcvar_mpc_launch_groups.argtypes = [modelp, i64, i64]
+    lib.drcvar_mpc_launch_groups.restype = ctypes.c_int32
     lib.drcvar_mpc_filter_f64.argtypes = [
         modelp, ptr, i64, ptr, ptr, i64, i64, i64, i64, i64, i64, i64, i64, ptr, i64, ptr, i64,
         i64, ptr, i64, i64, i32, dbl, i32, ptr, ptr, ptr, ptr, i64, ptr]

@@ -88,6 +88,11 @@ class MPCModel:
         self.A, self.B = A, B
         self.nx, self.nu, self.horizon = nx, nu, int(horizon)
 
+    def launch_groups(self, n_problems, n_obstacles):
+        """Workgroups per problem a launch of this batch shape uses (drcvar_mpc_launch_groups)."""
+        return int(_native.lib().drcvar_mpc_launch_groups(ctypes.byref(self.model), n_problems,
+                                                          n_obstacles))
+
     def workspace_doubles(self, n_problems, n_obstacles):
         return int(_native.lib().drcvar_mpc_workspace_doubles(ctypes.byref(self.model), n_problems,
                                                              n_obstacles))

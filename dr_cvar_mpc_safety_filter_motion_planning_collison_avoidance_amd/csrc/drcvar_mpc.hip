@@ -35,6 +35,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -124,7 +125,8 @@ struct MpcArgs {
   double* u_out;
   double* info;
   double* ws;
-  int64_t ws_pp;
+  int64_t ws_off, ws_pp;  // per-problem region b at ws + ws_off + b * ws_pp
+  int cl_size;            // workgroups per problem (clustered form)
   int max_iter;
   double tol;
   int polish;
@@ -1025,6 +1027,156 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
   return t;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Clusters: one large problem (a C5 hand-off: 12 800 halfspace rows) on several workgroups.
+// Every workgroup of a problem's cluster runs the whole interior-point method on its own — the
+// Riccati factorisation, the solves and every decision are replicated, bitwise identical — and
+// sweeps only its slice of the obstacles.  The row sums each sweep produces (per-step sums and a
+// few scalars) are exchanged between the cluster's workgroups and combined in workgroup order by
+// each of them, so every workgroup continues from the same totals and the solve stays
+// deterministic.  Nothing else crosses workgroups: no broadcast, no leader.
+// Exchange protocol (write-through payload, one counter per problem, no fences; the visibility
+// rules of the MI355X guide, hand-off form "one lane signals by an agent-scope atomic add"):
+//   wave 0 stores its workgroup's record with agent-scope (write-through) 8-B stores, drains them
+//   (s_waitcnt vmcnt(0)), lane 0 adds 1 to the problem's counter; wave 0 polls the counter with
+//   agent-scope loads until all `size` workgroups have arrived at this exchange, then every wave
+//   reads the records with agent-scope loads (they bypass the CU's L1).  Records alternate
+//   between two buffers: a workgroup can be at most one exchange ahead of the slowest reader.
+// Every spin is bounded (kSpinTicks of the 100 MHz clock); a workgroup that gives up adds
+// kAbortBias to the counter, which releases every wait of every workgroup at once, and the
+// problem ends NUMERICAL (the fallback rollout) instead of hanging the launch.  The counters are
+// zeroed by a one-wave kernel in front of every launch; the clustered launch never has more workgroups
+// than the device has CUs, and asks for more LDS than two workgroups can share, so each
+// workgroup has a CU of its own and all of them are resident.
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+constexpr int kRec = 512;                        // doubles per exchange record
+constexpr int kRecScalars = kPerStepQ * 64;      // [kPerStepQ][64] per-step sums, then scalars
+constexpr int kCtrlDoubles = 16;                 // 128-B control block per problem (the counter)
+constexpr int kClusterScratch = kMaxWaves * 4 + 8;  // LDS doubles of the exchange
+constexpr unsigned long long kAbortBias = 1ull << 40;
+constexpr uint64_t kSpinTicks = 5000000;         // 50 ms of s_memrealtime (100 MHz)
+enum { kOpSum = 0, kOpMax = 1, kOpMin = 2 };
+
+__device__ __forceinline__ double op_apply(int op, double a, double b) {
+  return op == kOpSum ? a + b : (op == kOpMax ? fmax(a, b) : fmin(a, b));
+}
+__device__ __forceinline__ double op_wave(int op, double v) {
+  return op == kOpSum ? wave_sum(v) : (op == kOpMax ? wave_max(v) : wave_min(v));
+}
+__device__ __forceinline__ double op_identity(int op) {
+  return op == kOpSum ? 0.0 : (op == kOpMax ? -INFINITY : INFINITY);
+}
+__device__ __forceinline__ void store_wt(double* p, double v) {  // write-through (sc1) 8-B store
+  __hip_atomic_store((gu64*)p, static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_wt(const double* p) {  // agent-scope load (bypasses L1)
+  return __longlong_as_double(static_cast<long long>(
+      __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+
+struct Cluster {
+  int size, id;     // workgroups per problem, this workgroup's index in its cluster
+  gu64* ctr;        // the problem's arrival counter
+  double* xbuf;     // [2][size][kRec] exchange records
+  double* cx;       // LDS scratch [kClusterScratch]
+  unsigned epoch;   // exchanges completed (the same count in every workgroup of the cluster)
+  bool aborted;     // a wait gave up (uniform after the exchange that saw it)
+};
+
+// Per-step values acc[q] (lane = step, this thread's rows) combined over the cluster with
+// step_op, and NS scalars sv[i] with ops[i]; on return s.red[q * 64 + lane] holds the cluster's
+// per-step totals and sv[i] the cluster's scalar totals (in every thread).  A sum counts every
+// thread's value once: callers pass row contributions only (max / min may include replicated
+// terms).  Contains barriers: every thread of the workgroup calls it.
+template <int kWaves, int Q, int NS>
+__device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* acc, int step_op,
+                                       double* sv, const int* ops) {
+  static_assert(Q < kWaves && NS <= 4, "exchange layout");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* cx = cl.cx;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const double v = op_wave(ops[i], sv[i]);
+    if (lane == 0) cx[i * kWaves + wave] = v;
+  }
+  __syncthreads();
+  const int64_t half = static_cast<int64_t>(cl.epoch & 1u) * cl.size * kRec;
+  if (wave == 0) {
+    double* rec = cl.xbuf + half + static_cast<int64_t>(cl.id) * kRec;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      double t = s.red[q * 64 + lane];
+      for (int w = 1; w < kWaves; ++w) t = op_apply(step_op, t, s.red[(w * kPerStepQ + q) * 64 + lane]);
+      store_wt(rec + q * 64 + lane, t);
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      if (lane == i) {
+        double t = cx[i * kWaves];
+        for (int w = 1; w < kWaves; ++w) t = op_apply(ops[i], t, cx[i * kWaves + w]);
+        store_wt(rec + kRecScalars + i, t);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is out before the arrival
+    if (lane == 0) __hip_atomic_fetch_add(cl.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = (static_cast<unsigned long long>(cl.epoch) + 1ull) * cl.size;
+    bool gave_up = false;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const unsigned long long seen = __hip_atomic_load(cl.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long v =
+          (static_cast<unsigned long long>(static_cast<unsigned>(
+               __builtin_amdgcn_readfirstlane(static_cast<int>(seen >> 32)))) << 32) |
+          static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(seen)));
+      if (v >= target) {
+        gave_up = v >= kAbortBias;
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // bounded: release everyone
+        if (lane == 0) __hip_atomic_fetch_add(cl.ctr, kAbortBias, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gave_up = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+    if (lane == 0) cx[kMaxWaves * 4] = gave_up ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  // the records of the cluster, combined in workgroup order (every workgroup: the same order)
+  const double* base = cl.xbuf + half;
+  if (wave < Q) {
+    double v[8];
+    double t = op_identity(step_op);
+    for (int c0 = 0; c0 < cl.size; c0 += 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        v[i] = c0 + i < cl.size ? load_wt(base + static_cast<int64_t>(c0 + i) * kRec + wave * 64 + lane)
+                                : op_identity(step_op);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t = op_apply(step_op, t, v[i]);
+    }
+    s.red[wave * 64 + lane] = t;
+  }
+  if (NS > 0 && wave == kWaves - 1) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double v = lane < cl.size ? load_wt(base + static_cast<int64_t>(lane) * kRec + kRecScalars + i)
+                                : op_identity(ops[i]);
+      v = op_wave(ops[i], v);
+      if (lane == 0) cx[kMaxWaves * 4 + 1 + i] = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NS; ++i) sv[i] = cx[kMaxWaves * 4 + 1 + i];
+  cl.aborted = cl.aborted || cx[kMaxWaves * 4] != 0.0;
+  ++cl.epoch;
+}
+
 // Row sweep of one thread (lane = halfspace step, obstacles o = wave, wave + kWaves, ...).  The
 // rows of kSweep obstacles are loaded together before any is processed.  With two waves per SIMD
 // in both kernel forms the other wave hides the row loads' latency, and a deeper sweep only adds
@@ -1032,15 +1184,15 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
 // no spills on the 4-state forms).  Inside the body: q (the row), o, r (its workspace index).
 constexpr int kSweep = 1;
 #define ROW_SWEEP_BEGIN                                                              \
-  for (int o0_ = wave; o0_ < O; o0_ += kSweep * kWaves) {                            \
+  for (int o0_ = o_lo + wave; o0_ < o_hi; o0_ += kSweep * kWaves) {                \
     HsRow qs_[kSweep];                                                               \
     _Pragma("unroll") for (int i_ = 0; i_ < kSweep; ++i_) {                          \
       const int o_ = o0_ + i_ * kWaves;                                              \
-      if (o_ < O) qs_[i_] = rows.load(static_cast<int64_t>(o_) * kRowStride + lane); \
+      if (o_ < o_hi) qs_[i_] = rows.load(static_cast<int64_t>(o_) * kRowStride + lane); \
     }                                                                                \
     _Pragma("unroll") for (int i_ = 0; i_ < kSweep; ++i_) {                          \
       const int o = o0_ + i_ * kWaves;                                               \
-      if (o >= O) break;                                                             \
+      if (o >= o_hi) break;                                                             \
       const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;                 \
       (void)r;                                                                       \
       const HsRow q = qs_[i_];
@@ -1051,18 +1203,36 @@ constexpr int kSweep = 1;
 // BLK threads per problem; HMX the horizon capacity of its LDS plan.  Every form targets two
 // waves per SIMD (HIP's second launch bound; VGPR budget 256): 512 and 256 threads with two
 // workgroups per CU, 128 threads with four.
-template <int NU, int NX, int BLK, int HMX>
+// CL: clustered form — a.cl_size workgroups per problem (grid = problems x cl_size), each
+// sweeping the obstacles [o_lo, o_hi) and exchanging row sums (cluster_combine).
+template <int NU, int NX, int BLK, int HMX, bool CL = false>
 __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   constexpr int kBlock = BLK;
   constexpr int kWaves = BLK / 64;
   static_assert(kWaves <= kMaxWaves, "LDS plan sized for kMaxWaves");
   extern __shared__ double lds_raw[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = blockIdx.x;
+  const int cl_size = CL ? a.cl_size : 1;
+  const int64_t b = blockIdx.x / cl_size;
+  const int cid = static_cast<int>(blockIdx.x - b * cl_size);
   const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
+  const int o_lo = CL ? static_cast<int>((static_cast<int64_t>(O) * cid) / cl_size) : 0;
+  const int o_hi = CL ? static_cast<int>((static_cast<int64_t>(O) * (cid + 1)) / cl_size) : O;
   const Lds s = carve<kWaves, NU, NX, HMX>(lds_raw);
   const double* H0 = a.blob + a.off.H0;
-  double* ws = a.ws + b * a.ws_pp;
+  double* ws = a.ws + a.ws_off + b * a.ws_pp;
+  Cluster cl{};
+  if constexpr (CL) {
+    cl.size = cl_size;
+    cl.id = cid;
+    cl.ctr = (gu64*)(a.ws + b * kCtrlDoubles);
+    cl.xbuf = ws + kRowArrays * static_cast<int64_t>(O) * kStepPad + static_cast<int64_t>(cl_size) * kBestPad;
+    cl.cx = lds_raw + LdsPlan<kWaves, NU, NX, HMX>::total;
+    cl.epoch = 0;
+    cl.aborted = false;
+  }
+  (void)cl;
+  (void)O;
 #ifdef DRCVAR_MPC_STAMPS
   unsigned long long stamp_acc[kStampSlots] = {};
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
@@ -1114,7 +1284,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   double gmax = 0.0;
   if (lane < K) {
     const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
-    for (int o = wave; o < O; o += kWaves) {
+    for (int o = o_lo + wave; o < o_hi; o += kWaves) {
       const double* hp = a.hs_h + b * a.h_sp + o * a.h_so + lane * a.h_sk;
       const double g = a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk];
       const double h0 = hp[0], h1 = hp[1];
@@ -1155,6 +1325,10 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   }
   double fmaxv = 0.0;
   for (int j = tid; j < n; j += kBlock) fmaxv = fmax(fmaxv, fabs(s.f[j]));
+  if constexpr (CL) {  // |g| over every workgroup's rows (the bound terms are replicated: max)
+    const int ops[1] = {kOpMax};
+    cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &gmax, ops);
+  }
   {
     double unused = 0.0;
     block_sum_max_max<kWaves>(unused, gmax, fmaxv, s.sc);
@@ -1167,7 +1341,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   int status = DRCVAR_MPC_STATUS_MAX_ITER;
   int it = 0, best_it = 0;
   double mu = 0.0, rp = 0.0, rd = 0.0, best_merit = kHuge;
-  double* best_u = ws + kRowArrays * pitch;  // [n] best iterate
+  double* best_u = ws + kRowArrays * pitch + static_cast<int64_t>(cid) * kBestPad;  // [n] best iterate
   // P1's row part — per-step sums of the weights / duals / affine rhs, the gap and the residual
   // maxima at positions (p0, p1) — accumulated by each thread for its rows.  It runs fused with
   // the previous iteration's update pass (P5): the rows are swept once per iteration less.
@@ -1209,13 +1383,23 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     // ---- P1: residuals, weights, per-step S / v / affine rhs (row sums already taken) ----
     {
       double gap = gap_rows, rpm = rpm_rows, rdm = rdm_rows;
+      if constexpr (CL) {  // the cluster's row sums; the gap total enters once (thread 0)
+        double sv[3] = {gap_rows, rpm_rows, rdm_rows};
+        const int ops[3] = {kOpSum, kOpMax, kOpMax};
+        cluster_combine<kWaves, kPerStepQ, 3>(cl, s, acc, kOpSum, sv, ops);
+        gap = tid == 0 ? sv[0] : 0.0;
+        rpm = sv[1];
+        rdm = sv[2];
+      } else {
 #pragma unroll
-      for (int q = 0; q < kPerStepQ; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
-      __syncthreads();
+        for (int q = 0; q < kPerStepQ; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+        __syncthreads();
+      }
       if (wave == 0 && lane < H) {
         double tot[kPerStepQ];
 #pragma unroll
-        for (int q = 0; q < kPerStepQ; ++q) tot[q] = lane < K ? step_total<kWaves>(s.red, q, lane) : 0.0;
+        for (int q = 0; q < kPerStepQ; ++q)
+          tot[q] = lane < K ? (CL ? s.red[q * 64 + lane] : step_total<kWaves>(s.red, q, lane)) : 0.0;
         if (a.has_p) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -1334,10 +1518,20 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
           acc[3] += cu * q.h1;
         ROW_SWEEP_END
       }
-      // published by the barriers of block_min below (positions' reads of s.red ended at the
-      // barrier before this sweep)
+      if constexpr (CL) {  // the cluster's rows: step length (min), gap quadratic, rhs sums
+        double sv[4] = {amax, gq0, gq1, gq2};
+        const int ops[4] = {kOpMin, kOpSum, kOpSum, kOpSum};
+        cluster_combine<kWaves, 4, 4>(cl, s, acc, kOpSum, sv, ops);
+        amax = sv[0];
+        gq0 = tid == 0 ? sv[1] : 0.0;  // the quadratic enters the block sum once
+        gq1 = tid == 0 ? sv[2] : 0.0;
+        gq2 = tid == 0 ? sv[3] : 0.0;
+      } else {
+        // published by the barriers of block_min below (positions' reads of s.red ended at the
+        // barrier before this sweep)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+        for (int q = 0; q < 4; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+      }
       if (a.has_u) {
         for (int j = tid; j < n; j += kBlock) {
           const int ai = j % NU;
@@ -1359,7 +1553,8 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
       if (wave == 0 && lane < H) {
         double tot[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tot[q] = lane < K ? step_total<kWaves>(s.red, q, lane) : 0.0;
+        for (int q = 0; q < 4; ++q)
+          tot[q] = lane < K ? (CL ? s.red[q * 64 + lane] : step_total<kWaves>(s.red, q, lane)) : 0.0;
         if (a.has_p) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -1426,6 +1621,10 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         const HsLin l = hs_lin(q, p0, p1);
         amax = fmin(amax, hs_ratio(q, hs_corrector(q, l, q.h0 * a0 + q.h1 * a1, q.h0 * d0 + q.h1 * d1, sigma_mu)));
       ROW_SWEEP_END
+    }
+    if constexpr (CL) {
+      const int ops[1] = {kOpMin};
+      cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &amax, ops);
     }
     if (a.has_u) {
       for (int j = tid; j < n; j += kBlock) {
@@ -1536,7 +1735,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     // classify: flag 0 = halfspace not binding (s = 0), 1 = slack positive (s = h.p + g > 0),
     // 2 = binding with s = 0 (equality, multiplier nu in [0, 50]); rows.s <- nu, rows.wA <- flag
     if (lane < K) {
-      for (int o = wave; o < O; o += kWaves) {
+      for (int o = o_lo + wave; o < o_hi; o += kWaves) {
         const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
         const bool actA = rows.lA[r] > rows.wA[r], actB = rows.lB[r] > rows.wB[r];
         const double flag = actA ? (actB ? 2.0 : 1.0) : 0.0;
@@ -1573,7 +1772,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
       {
         double acc[3] = {0, 0, 0};
         if (lane < K) {
-          for (int o = wave; o < O; o += kWaves) {
+          for (int o = o_lo + wave; o < o_hi; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             const double flag = rows.wA[r];
             const double wgt = flag == 1.0 ? kSlackHess : (flag == 2.0 ? kPolishRho : 0.0);
@@ -1583,13 +1782,17 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
             acc[2] += wgt * h1 * h1;
           }
         }
+        if constexpr (CL) {
+          cluster_combine<kWaves, 3, 0>(cl, s, acc, kOpSum, nullptr, nullptr);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
-        __syncthreads();
+          for (int q = 0; q < 3; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
+          __syncthreads();
+        }
         if (wave == 0 && lane < H) {
-          double t0 = lane < K ? step_total<kWaves>(s.red, 0, lane) : 0.0;
-          const double t1 = lane < K ? step_total<kWaves>(s.red, 1, lane) : 0.0;
-          double t2 = lane < K ? step_total<kWaves>(s.red, 2, lane) : 0.0;
+          double t0 = lane < K ? (CL ? s.red[lane] : step_total<kWaves>(s.red, 0, lane)) : 0.0;
+          const double t1 = lane < K ? (CL ? s.red[64 + lane] : step_total<kWaves>(s.red, 1, lane)) : 0.0;
+          double t2 = lane < K ? (CL ? s.red[128 + lane] : step_total<kWaves>(s.red, 2, lane)) : 0.0;
           if (a.has_p) {
             t0 += kPolishRho * (s.px[2 * lane] + s.px[4 * H + 2 * lane]);
             t2 += kPolishRho * (s.px[2 * lane + 1] + s.px[4 * H + 2 * lane + 1]);
@@ -1610,7 +1813,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         double acc[2] = {0, 0};
         if (lane < K) {
           const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
-          for (int o = wave; o < O; o += kWaves) {
+          for (int o = o_lo + wave; o < o_hi; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             const double flag = rows.wA[r];
             const double h0 = rows.h0[r], h1 = rows.h1[r];
@@ -1621,14 +1824,18 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
             acc[1] += coef * h1;
           }
         }
-        s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];
-        s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
-        __syncthreads();
+        if constexpr (CL) {
+          cluster_combine<kWaves, 2, 0>(cl, s, acc, kOpSum, nullptr, nullptr);
+        } else {
+          s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];
+          s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
+          __syncthreads();
+        }
         if (wave == 0 && lane < H) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const int t = 2 * lane + i;
-            double z = lane < K ? step_total<kWaves>(s.red, i, lane) : 0.0;
+            double z = lane < K ? (CL ? s.red[i * 64 + lane] : step_total<kWaves>(s.red, i, lane)) : 0.0;
             if (a.has_p) {
               if (s.px[t] != 0.0) z += s.px[2 * H + t] - kPolishRho * (a.pmax[i] - s.c[t]);
               if (s.px[4 * H + t] != 0.0) z -= s.px[6 * H + t] - kPolishRho * (s.c[t] - a.pmin[i]);
@@ -1660,7 +1867,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         double eres = 0.0;
         if (lane < K) {
           const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-          for (int o = wave; o < O; o += kWaves) {
+          for (int o = o_lo + wave; o < o_hi; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             if (rows.wA[r] == 2.0) {
               const double e = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
@@ -1697,6 +1904,10 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         }
         // The multipliers have converged once the equalities hold to roundoff (a further pass
         // moves nu by rho * eres and u by ~eres): stop instead of running all kPolishIters.
+        if constexpr (CL) {  // every workgroup's equality rows (the bound terms: replicated)
+          const int ops[1] = {kOpMax};
+          cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &eres, ops);
+        }
         double unused_a = 0.0, unused_b = 0.0;
         block_sum_max_max<kWaves>(unused_a, eres, unused_b, s.sc);  // uniform; also the barrier
         if (eres <= kPolishEqTol * scale_d) break;
@@ -1712,7 +1923,7 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
         double vmax = 0.0, dmax = 0.0;
         if (lane < K) {
           const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-          for (int o = wave; o < O; o += kWaves) {
+          for (int o = o_lo + wave; o < o_hi; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
             const double flag = rows.wA[r];
             const double hp = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
@@ -1720,18 +1931,28 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
             dmax = fmax(dmax, flag == 2.0 ? -rows.s[r] : 0.0);
           }
         }
-        s.red[(wave * kPerStepQ) * 64 + lane] = vmax;
-        s.red[(wave * kPerStepQ + 1) * 64 + lane] = dmax;
+        if constexpr (CL) {  // per-step maxima over the cluster's rows
+          const double vm[2] = {vmax, dmax};
+          cluster_combine<kWaves, 2, 0>(cl, s, vm, kOpMax, nullptr, nullptr);
+        } else {
+          s.red[(wave * kPerStepQ) * 64 + lane] = vmax;
+          s.red[(wave * kPerStepQ + 1) * 64 + lane] = dmax;
+          __syncthreads();
+        }
       }
-      __syncthreads();
       if (lane < K) {
         double step_vmax = 0.0, step_dmax = 0.0;
-        for (int w = 0; w < kWaves; ++w) {
-          step_vmax = fmax(step_vmax, s.red[(w * kPerStepQ) * 64 + lane]);
-          step_dmax = fmax(step_dmax, s.red[(w * kPerStepQ + 1) * 64 + lane]);
+        if constexpr (CL) {
+          step_vmax = s.red[lane];
+          step_dmax = s.red[64 + lane];
+        } else {
+          for (int w = 0; w < kWaves; ++w) {
+            step_vmax = fmax(step_vmax, s.red[(w * kPerStepQ) * 64 + lane]);
+            step_dmax = fmax(step_dmax, s.red[(w * kPerStepQ + 1) * 64 + lane]);
+          }
         }
         const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-        for (int o = wave; o < O; o += kWaves) {
+        for (int o = o_lo + wave; o < o_hi; o += kWaves) {
           const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
           const double flag = rows.wA[r];
           const double hp = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
@@ -1757,6 +1978,11 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
           rows.wA[r] = nf;
           rows.s[r] = nv;
         }
+      }
+      if constexpr (CL) {  // unresolved rows of the whole cluster, counted once (thread 0)
+        const int ops[1] = {kOpSum};
+        cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &bad, ops);
+        bad = tid == 0 ? bad : 0.0;
       }
       if (a.has_u) {
         for (int j = tid; j < n; j += kBlock) {
@@ -1799,6 +2025,9 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
 
   MPC_PHASE(7);
   // ------------------------------- output -------------------------------
+  if constexpr (CL) {
+    if (cl.aborted) status = DRCVAR_MPC_STATUS_NUMERICAL;  // a cluster wait gave up: fallback
+  }
   const bool optimal = status == DRCVAR_MPC_STATUS_OPTIMAL || status == DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
   if (!optimal) {
     const double* uf = a.uf + b * a.uf_sp;
@@ -1829,7 +2058,8 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
   }
   __syncthreads();
   // objective (core/mpc_filter.py:64-76,142-144) and the largest slack
-  double obj = 0.0, smax = 0.0;
+  double obj = 0.0, smax = 0.0, obj_rows = 0.0;
+  double& obj_hs = CL ? obj_rows : obj;  // the rows' terms (clustered: summed over the cluster)
   if (optimal) {
     const double* Q = a.blob + a.off.Q;
     const double* R = a.blob + a.off.R;
@@ -1850,14 +2080,23 @@ __global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
     if (lane < K) {
       // the optimal slack of a halfspace for the returned inputs is max(0, h.p + g)
       const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
-      for (int o = wave; o < O; o += kWaves) {
+      for (int o = o_lo + wave; o < o_hi; o += kWaves) {
         const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
         const double sv = fmax(0.0, rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r]);
         rows.s[r] = sv;
-        obj += kSlackLin * sv + 0.5 * kSlackHess * sv * sv;
+        obj_hs += kSlackLin * sv + 0.5 * kSlackHess * sv * sv;
         smax = fmax(smax, sv);
       }
     }
+  }
+  if constexpr (CL) {
+    double sv[2] = {obj_rows, smax};
+    const int ops[2] = {kOpSum, kOpMax};
+    cluster_combine<kWaves, 0, 2>(cl, s, nullptr, kOpSum, sv, ops);
+    obj += tid == 0 ? sv[0] : 0.0;
+    smax = sv[1];
+    if (cl.aborted) status = DRCVAR_MPC_STATUS_NUMERICAL;
+    if (cid != 0) return;  // workgroup 0 writes the problem's outputs (every one holds them)
   }
   double unused = 0.0;
   block_sum_max_max<kWaves>(obj, smax, unused, s.sc);
@@ -1895,19 +2134,71 @@ bool all_finite(const double* p, int64_t n) {
   return true;
 }
 
-template <int NU, int NX, int BLK, int HMX = DRCVAR_MPC_MAX_HORIZON>
+// Clustered launches (a few large problems): workgroups per problem.  One obstacle per wave of
+// the 512-thread form at the most (8 per workgroup), at most kClusterMax workgroups per problem
+// and never more workgroups in all than CUs.  Problems with fewer than kClusterMinObstacles
+// obstacles (≤ 8 rows per thread on one workgroup) stay on one workgroup: the exchanges
+// (~3 per interior-point iteration) would cost more than the sweeps they split.
+constexpr int kClusterMaxProblems = 8;
+constexpr int kClusterMinObstacles = 64;
+constexpr int kClusterObstaclesPerGroup = 8;
+constexpr int kClusterMax = 32;
+constexpr int kClusterCUs = 256;  // workspace sizing; launches use the device's own CU count
+
+int cluster_size(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
+  if (n_problems < 1 || n_problems > kClusterMaxProblems || n_obstacles < kClusterMinObstacles) return 1;
+  int64_t c = (n_obstacles + kClusterObstaclesPerGroup - 1) / kClusterObstaclesPerGroup;
+  c = c < kClusterMax ? c : kClusterMax;
+  c = c < cus / n_problems ? c : cus / n_problems;
+  return c < 2 ? 1 : static_cast<int>(c);
+}
+
+// zeroes the per-problem arrival counters of a clustered launch (in front of it, same stream)
+__global__ void zero_counters_kernel(double* ws, int n_problems) {
+  for (int b = threadIdx.x; b < n_problems; b += blockDim.x)
+    __hip_atomic_store((gu64*)(ws + b * kCtrlDoubles), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// DRCVAR_MPC_CLUSTER=<c> caps the workgroups per problem (1: the one-workgroup form); A/B runs
+int cluster_cap() {
+  const char* e = std::getenv("DRCVAR_MPC_CLUSTER");
+  if (!e || !*e) return kClusterMax;
+  const int v = std::atoi(e);
+  return v < 1 ? 1 : v;
+}
+
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  static int cached[64] = {};
+  if (dev >= 0 && dev < 64 && cached[dev] > 0) return cached[dev];
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (dev >= 0 && dev < 64) cached[dev] = cus;
+  return cus;
+}
+
+template <int NU, int NX, int BLK, int HMX = DRCVAR_MPC_MAX_HORIZON, bool CL = false>
 int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  constexpr size_t lds_bytes = sizeof(double) * LdsPlan<BLK / 64, NU, NX, HMX>::total;
+  // the clustered form asks for more LDS than two workgroups can share: one workgroup per CU
+  constexpr size_t plan_bytes = sizeof(double) * (LdsPlan<BLK / 64, NU, NX, HMX>::total + (CL ? kClusterScratch : 0));
+  constexpr size_t lds_bytes = CL && plan_bytes < 96 * 1024 ? 96 * 1024 : plan_bytes;
   static bool attr_set = false;  // idempotent; a racing second call sets the same value
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK, HMX>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK, HMX, CL>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK, HMX>), dim3(static_cast<unsigned>(n_problems)),
-                     dim3(BLK), lds_bytes, stream, args);
+  // the arrival counters, zeroed in front of every launch by a one-wave kernel of agent-scope
+  // (write-through) stores: a hipMemsetAsync node replayed from a hipGraph left the counters
+  // unreliable from the second replay on (replays 2..5 timed out or read garbage sums; with this
+  // kernel every replay reproduced the eager launch, scripts/micro/cluster_graph_diag.py)
+  if constexpr (CL)
+    hipLaunchKernelGGL(zero_counters_kernel, dim3(1), dim3(64), 0, stream, args.ws, static_cast<int>(n_problems));
+  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK, HMX, CL>),
+                     dim3(static_cast<unsigned>(n_problems * (CL ? args.cl_size : 1))), dim3(BLK),
+                     lds_bytes, stream, args);
   return DRCVAR_OK;
 }
 
@@ -1920,6 +2211,9 @@ int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
   // form.
   const bool few = n_problems <= kFewProblems;
   const bool short_h = args.H <= kShortHorizon;
+  if (args.cl_size > 1)
+    return args.nx <= 4 ? launch<NU, 4, 512, DRCVAR_MPC_MAX_HORIZON, true>(args, n_problems, stream)
+                        : launch<NU, 8, 512, DRCVAR_MPC_MAX_HORIZON, true>(args, n_problems, stream);
   if (args.nx <= 4)
     return few ? launch<NU, 4, 512>(args, n_problems, stream)
                : short_h ? launch<NU, 4, 128, kShortHorizon>(args, n_problems, stream)
@@ -2064,7 +2358,25 @@ int drcvar_mpc_model_init(const double* A, const double* B, const double* C, con
 int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_problems,
                                      int64_t n_obstacles) {
   if (!model || n_problems < 0 || n_obstacles < 0) return -1;
-  return n_problems * (kRowArrays * n_obstacles * kStepPad + kBestPad);
+  const int c = cluster_size(n_problems, n_obstacles, kClusterCUs);
+  if (c == 1) return n_problems * (kRowArrays * n_obstacles * kStepPad + kBestPad);
+  // clustered: the counters first, then per problem the rows, a best iterate per workgroup and
+  // the two exchange buffers
+  return n_problems * (kCtrlDoubles + kRowArrays * n_obstacles * kStepPad +
+                       static_cast<int64_t>(c) * (kBestPad + 2 * kRec));
+}
+
+int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,
+                                 int64_t n_obstacles) {
+  if (!model || n_problems < 0 || n_obstacles < 0) return -1;
+  const int c_ws = cluster_size(n_problems, n_obstacles, kClusterCUs);
+  if (c_ws == 1) return 1;
+  const int cus = device_cus();
+  int c = cluster_size(n_problems, n_obstacles, cus > 0 ? cus : 1);
+  c = c < c_ws ? c : c_ws;
+  const int cap = cluster_cap();
+  c = c < cap ? c : cap;
+  return c < 2 ? 1 : c;
 }
 
 int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
@@ -2129,7 +2441,15 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
   args.u_out = u_out;
   args.info = info_out;
   args.ws = workspace;
+  args.ws_off = 0;
   args.ws_pp = kRowArrays * n_obstacles * kStepPad + kBestPad;
+  args.cl_size = 1;
+  const int c_ws = cluster_size(n_problems, n_obstacles, kClusterCUs);
+  if (c_ws > 1) {  // the workspace is laid out for c_ws; a smaller device or the cap uses fewer
+    args.ws_off = kCtrlDoubles * n_problems;
+    args.ws_pp = kRowArrays * n_obstacles * kStepPad + static_cast<int64_t>(c_ws) * (kBestPad + 2 * kRec);
+    args.cl_size = drcvar_mpc_launch_groups(model, n_problems, n_obstacles);
+  }
   args.max_iter = max_iter;
   args.tol = tol;
   args.polish = polish;

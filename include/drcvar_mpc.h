@@ -85,9 +85,21 @@ int drcvar_mpc_model_init(const double* A, const double* B, const double* C, con
                           const double* p_min, const double* p_max, drcvar_mpc_model* model,
                           double* blob);
 
-/* Doubles of device workspace drcvar_mpc_filter_f64 needs for this batch. */
+/* Doubles of device workspace drcvar_mpc_filter_f64 needs for this batch (clustered shapes, see
+ * drcvar_mpc_launch_groups, also hold per-problem arrival counters at the workspace's start and
+ * exchange buffers; the launch zeroes the counters itself). */
 int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_problems,
                                      int64_t n_obstacles);
+
+/*
+ * Workgroups per problem the next drcvar_mpc_filter_f64 launch of this batch shape uses on the
+ * current device: 1 (one workgroup per problem), or a cluster of c > 1 workgroups that split the
+ * problem's halfspace rows (batches of at most 8 problems with >= 64 obstacles; c <= 32 and
+ * c * n_problems <= the device's CUs; environment DRCVAR_MPC_CLUSTER=<c> caps it, 1 disables).
+ * Host query (reads the device's CU count).  -1 on invalid arguments.
+ */
+int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,
+                                 int64_t n_obstacles);
 
 /*
  * Solve n_problems independent safety-filter QPs.

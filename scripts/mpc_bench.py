@@ -66,7 +66,8 @@ def main():
         ms = t0.elapsed_time(t1) / args.reps
         inf = info.cpu().numpy()
         st = inf[:, _native.MPC_INFO_STATUS]
-        print(f"H={H} O={O} B={B}: {ms:.3f} ms/launch, {B / ms * 1e3:.0f} QPs/s, "
+        print(f"H={H} O={O} B={B} groups={model.launch_groups(B, O)}: {ms:.3f} ms/launch, "
+              f"{B / ms * 1e3:.0f} QPs/s, "
               f"iters {inf[:, _native.MPC_INFO_ITERATIONS].mean():.1f}, "
               f"polished {inf[:, _native.MPC_INFO_POLISHED].mean():.2f}, "
               f"optimal {(st == 0).mean():.2f}, fallback {inf[:, _native.MPC_INFO_USED_FALLBACK].mean():.2f}",

@@ -1,0 +1,168 @@
+"""Clustered QP launches (csrc/drcvar_mpc.hip, cluster_combine): one large safety-filter problem
+(core/mpc_filter.py:116-151 with many obstacles, e.g. the C5 hand-off's 12 800 halfspace rows) on
+several workgroups that split the rows and exchange their row sums inside the launch.
+
+CPU: the workspace layout of clustered shapes.  GPU: clustered launches against the oracle
+(oracle/mpc_qp.py, KKT-certified) and against the one-workgroup form (DRCVAR_MPC_CLUSTER=1) —
+C5 hand-off shape, uneven obstacle slices, several problems per launch, every cluster size cap,
+run-to-run bitwise determinism and hipGraph capture/replay (a one-wave kernel re-zeroes the
+counters in front of every replay).  Tolerance as tests/test_mpc.py: MPC_TOL on inputs and states.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
+from test_mpc import MPC_TOL, _oracle, _random_problem, double_integrator, model_init
+
+CTRL, ROWS, BEST, REC = 16, 8 * 64, 128, 512
+
+
+@pytest.mark.parametrize("B,O,groups", [(1, 256, 32), (1, 64, 8), (3, 100, 13), (8, 70, 9),
+                                        (1, 1000, 32), (9, 256, 1), (1, 63, 1), (2, 512, 32)])
+def test_cluster_workspace_layout(B, O, groups):
+    A, Bm, C = double_integrator()
+    _, m, _ = model_init(A, Bm, C, 2 * np.eye(4), np.eye(2), 50, blob=False)
+    ws = _native.lib().drcvar_mpc_workspace_doubles(ctypes.byref(m), B, O)
+    if groups == 1:
+        assert ws == B * (ROWS * O + BEST)
+    else:
+        assert ws == B * (CTRL + ROWS * O + groups * (BEST + 2 * REC))
+
+
+@pytest.fixture()
+def cluster_cap(monkeypatch):
+    def set_cap(c):
+        if c is None:
+            monkeypatch.delenv("DRCVAR_MPC_CLUSTER", raising=False)
+        else:
+            monkeypatch.setenv("DRCVAR_MPC_CLUSTER", str(c))
+    return set_cap
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _batch(dyn, H, O, B, tight, seed):
+    """B problems of one model (same dynamics / bounds), each with its own halfspaces and path."""
+    rng = np.random.default_rng(seed)
+    base = _random_problem(rng, O, H, H, dyn, True, tight)
+    probs = []
+    for _ in range(B):
+        other = _random_problem(rng, O, H, H, dyn if dyn in ("double", "single") else "double",
+                                True, tight)
+        pr = dict(base)
+        pr["x0"] = np.zeros_like(base["x0"])
+        pr["x0"][:2] = other["x0"][:2]
+        pr["x_ref"] = np.zeros_like(base["x_ref"])
+        pr["x_ref"][:, :2] = other["x_ref"][:, :2]
+        pr["hs"] = other["hs"]
+        probs.append(pr)
+    return probs
+
+
+def _solve(probs, dev):
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    p0 = probs[0]
+    model = mf.MPCModel(p0["A"], p0["B"], p0["C"], p0["Q"], p0["R"], p0["H"], p0["ub"], p0["pb"],
+                        device=dev)
+    T_ = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    hs = T_(np.stack([p["hs"] for p in probs]))
+    x, u, info = mf.filter_batch(model, hs[..., 0:2], hs[..., 2], T_(np.stack([p["x0"] for p in probs])),
+                                 T_(np.stack([p["x_ref"] for p in probs])),
+                                 T_(np.stack([p["u_ref"] for p in probs])))
+    groups = model.launch_groups(len(probs), hs.shape[1])
+    return x.cpu().numpy(), u.cpu().numpy(), info.cpu().numpy(), groups
+
+
+def _check_vs_oracle(probs, x, u, info, label):
+    ok = (_native.MPC_STATUS_OPTIMAL, _native.MPC_STATUS_OPTIMAL_INACCURATE)
+    for b, pr in enumerate(probs):
+        assert int(info[b, _native.MPC_INFO_STATUS]) in ok, (label, b, info[b])
+        assert info[b, _native.MPC_INFO_USED_FALLBACK] == 0, (label, b)
+        xo, uo, io = _oracle(pr)
+        assert io["status"] == "optimal"
+        tol = MPC_TOL if info[b, _native.MPC_INFO_POLISHED] == 1 else 1e-5
+        np.testing.assert_allclose(u[b], uo, atol=tol, err_msg=f"{label} problem {b}")
+        np.testing.assert_allclose(x[b], xo, atol=tol, err_msg=f"{label} problem {b}")
+        if info[b, _native.MPC_INFO_POLISHED] == 1:
+            assert abs(info[b, _native.MPC_INFO_OBJECTIVE] - io["objective"]) <= 1e-6 * max(1.0, abs(io["objective"]))
+            assert abs(info[b, _native.MPC_INFO_MAX_SLACK] - max(io["slacks"].max(initial=0.0), 0.0)) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dyn,H,O,B,tight", [
+    ("double", 50, 256, 1, False),   # the C5 hand-off shape: 12 800 rows, 32 workgroups
+    ("double", 30, 100, 3, True),    # uneven slices (100 obstacles over 13 workgroups), 3 problems
+    ("single", 40, 64, 2, True),     # the smallest clustered shape
+    ("generic3", 24, 130, 1, True),  # three inputs, padded state template
+    ("double", 20, 70, 8, True),     # the largest clustered batch
+    ("generic8", 16, 90, 1, True),   # the 8-state template
+])
+def test_gpu_cluster_matches_oracle_and_one_workgroup(dyn, H, O, B, tight, dev, cluster_cap):
+    probs = _batch(dyn, H, O, B, tight, seed=H * 1000 + O + B)
+    cluster_cap(None)
+    x, u, info, groups = _solve(probs, dev)
+    assert groups > 1
+    _check_vs_oracle(probs, x, u, info, f"cluster x{groups}")
+    x2, u2, info2, _ = _solve(probs, dev)  # run to run: the same bits
+    np.testing.assert_array_equal(u, u2)
+    np.testing.assert_array_equal(x, x2)
+    np.testing.assert_array_equal(info, info2)
+    cluster_cap(1)
+    x1, u1, info1, g1 = _solve(probs, dev)
+    assert g1 == 1
+    _check_vs_oracle(probs, x1, u1, info1, "one workgroup")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [2, 3, 5, 16, 31])
+def test_gpu_cluster_every_size(cap, dev, cluster_cap):
+    """The same C5-shaped problem on clusters of 2..31 workgroups (slices of 8 to 128 obstacles)."""
+    probs = _batch("double", 50, 256, 1, False, seed=5)
+    cluster_cap(cap)
+    x, u, info, groups = _solve(probs, dev)
+    assert groups == cap
+    _check_vs_oracle(probs, x, u, info, f"cluster x{cap}")
+
+
+@pytest.mark.gpu
+def test_gpu_cluster_graph_replay(dev, cluster_cap):
+    """Captured in a hipGraph (the counters' zeroing kernel + the clustered kernel) and replayed
+    five times: every replay reproduces the eager launch bit for bit (a captured hipMemsetAsync
+    of the counters failed from the second replay on)."""
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    cluster_cap(None)
+    probs = _batch("double", 50, 256, 2, False, seed=9)
+    p0 = probs[0]
+    model = mf.MPCModel(p0["A"], p0["B"], p0["C"], p0["Q"], p0["R"], p0["H"], p0["ub"], p0["pb"],
+                        device=dev)
+    T_ = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    hs = T_(np.stack([p["hs"] for p in probs]))
+    args = (model, hs[..., 0:2], hs[..., 2], T_(np.stack([p["x0"] for p in probs])),
+            T_(np.stack([p["x_ref"] for p in probs])), T_(np.stack([p["u_ref"] for p in probs])))
+    ws = torch.empty(model.workspace_doubles(2, hs.shape[1]), dtype=torch.float64, device=dev)
+    assert model.launch_groups(2, hs.shape[1]) > 1
+    x_e, u_e, i_e = (t.clone() for t in mf.filter_batch(*args, workspace=ws))
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        mf.filter_batch(*args, workspace=ws)  # warm-up on the capture stream
+    torch.cuda.current_stream(dev).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = mf.filter_batch(*args, workspace=ws)
+    for _ in range(5):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], x_e) and torch.equal(out[1], u_e) and torch.equal(out[2], i_e)
+    _check_vs_oracle(probs, x_e.cpu().numpy(), u_e.cpu().numpy(), i_e.cpu().numpy(), "graph")
