@@ -94,8 +94,9 @@ int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_pr
 /*
  * Workgroups per problem the next drcvar_mpc_filter_f64 launch of this batch shape uses on the
  * current device: 1 (one workgroup per problem), or a cluster of c > 1 workgroups that split the
- * problem's halfspace rows (batches of at most 8 problems with >= 64 obstacles; c <= 32 and
- * c * n_problems <= the device's CUs; environment DRCVAR_MPC_CLUSTER=<c> caps it, 1 disables).
+ * problem's halfspace rows (batches of at most 8 problems with >= 64 obstacles: one workgroup per
+ * 16 obstacles, c <= 32 and c * n_problems <= the device's CUs; the environment variable
+ * DRCVAR_MPC_CLUSTER=<c> sets c within those limits, 1 selects the one-workgroup form).
  * Host query (reads the device's CU count).  -1 on invalid arguments.
  */
 int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,

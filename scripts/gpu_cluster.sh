@@ -22,3 +22,4 @@ run bench_cl 200 python -u scripts/mpc_bench.py --shapes $SHAPES
 DRCVAR_MPC_CLUSTER=1 run bench_one 200 python -u scripts/mpc_bench.py --shapes $SHAPES
 run mpc_tests 600 python -u -m pytest tests/test_mpc.py -m gpu -x -q --timeout 120 --timeout-method thread
 grep -h "ms/launch" $OUT/bench_cl.log $OUT/bench_one.log
+MPC_SHAPES="50,256,1 30,3,1" timeout -k 10 400 bash scripts/gpu_mpc_stamps.sh > $OUT/stamps.log 2>&1; tail -42 $OUT/stamps.log

@@ -283,8 +283,8 @@ __device__ inline Lds carve(double* base) {
 // ---- reductions (butterflies: every lane ends with the bitwise-identical value) ----
 // DPP row permutations (each an involution: quad xor 1, quad xor 2, half mirror, mirror) combine
 // within rows of 16 lanes, then the gfx950 lane swaps (permlane16 / permlane32) combine the rows;
-// no LDS on the chain (the __shfl_xor butterfly is six ds_bpermute round trips).  Every lane of
-// the wave must be active.
+// no LDS on the chain (the __shfl_xor butterfly these replace was six ds_bpermute round trips).
+// Every lane of the wave must be active.
 template <int CTRL>
 __device__ __forceinline__ double dpp_row_f64(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
@@ -309,17 +309,7 @@ __device__ __forceinline__ double wave_butterfly(double v, F op) {
   }
   return v;
 }
-// The interior-point block sums keep the xor butterfly (distances 32, 16, ..., 1): the DPP tree
-// associates the sum differently, and that rounding was enough to turn one degenerate test
-// instance (generic1, H = 64, more binding rows than inputs) from a successful polish into an
-// OPTIMAL_INACCURATE answer.  Max / min are exact in any order and take the DPP form; the cluster
-// exchange's sums (a new code path) take the DPP form too.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-  return v;
-}
-__device__ __forceinline__ double wave_sum_dpp(double v) {
   return wave_butterfly(v, [](double a, double b) { return a + b; });
 }
 __device__ __forceinline__ double wave_max(double v) {
@@ -1135,8 +1125,12 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 constexpr int kClusterMaxProblems = 8;
 constexpr int kClusterMinObstacles = 64;
-constexpr int kClusterObstaclesPerGroup = 16;  // C5: 16 workgroups (8..32 measured within 4 %)
+constexpr int kClusterObstaclesPerGroup = 8;
 constexpr int kClusterMax = 32;
+#ifndef DRCVAR_GATHER_BATCH
+#define DRCVAR_GATHER_BATCH 4
+#endif
+constexpr int kGatherBatch = DRCVAR_GATHER_BATCH;  // 16-B record loads in flight per lane
 constexpr int kClusterCUs = 256;  // workspace sizing; launches use the device's own CU count
 constexpr int kRec = 512;                        // doubles per exchange record
 constexpr int kRecScalars = kPerStepQ * 64;      // [kPerStepQ][64] per-step sums, then scalars
@@ -1150,7 +1144,7 @@ __device__ __forceinline__ double op_apply(int op, double a, double b) {
   return op == kOpSum ? a + b : (op == kOpMax ? fmax(a, b) : fmin(a, b));
 }
 __device__ __forceinline__ double op_wave(int op, double v) {
-  return op == kOpSum ? wave_sum_dpp(v) : (op == kOpMax ? wave_max(v) : wave_min(v));
+  return op == kOpSum ? wave_sum(v) : (op == kOpMax ? wave_max(v) : wave_min(v));
 }
 __device__ __forceinline__ double op_identity(int op) {
   return op == kOpSum ? 0.0 : (op == kOpMax ? -INFINITY : INFINITY);
@@ -1181,7 +1175,7 @@ struct Cluster {
 template <int kWaves, int Q, int NS>
 __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* acc, int step_op,
                                        double* sv, const int* ops) {
-  static_assert(Q < kWaves && NS <= 4, "exchange layout");
+  static_assert(Q < kWaves && NS <= 4 && kClusterMax <= 32, "exchange layout (gather: 2 x 16 records)");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* cx = cl.cx;
 #ifdef DRCVAR_MPC_STAMPS
@@ -1248,23 +1242,46 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   }
   __syncthreads();
   CL_STAMP(4);  // barrier after the poll
-  // Gather: wave q sums quantity q (lane = step) over the records in workgroup order, eight
-  // agent-scope loads in flight at a time — the same order in every workgroup of the cluster; the
-  // last wave gathers the scalars (lane = record).  (16-B loads of step pairs, two halves of the
-  // records per wave, measured slower: the extra live registers spilled.)
+  // Gather, every record with agent-scope 16-B loads: wave q, lane l sums quantity q of steps
+  // (2p, 2p + 1), p = l mod 32, over the records of its half (lanes < 32: records 0..15, the others
+  // 16..31), in record order; the halves are added through permlane32 — a fixed order, the same in
+  // every workgroup of the cluster.  The last wave gathers the scalars (lane = record).
   const double* base = cl.xbuf + half;
   if (wave < Q) {
-    double v[8];
-    double t = op_identity(step_op);
-    for (int c0 = 0; c0 < cl.size; c0 += 8) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0,
+                                                      cl.size * kRec * static_cast<int>(sizeof(double)), 0x00020000);
+    const int hrec = lane >> 5, pr = lane & 31;
+    double ta = op_identity(step_op), tb = ta;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        v[i] = c0 + i < cl.size ? load_wt(base + static_cast<int64_t>(c0 + i) * kRec + wave * 64 + lane)
-                                : op_identity(step_op);
+    for (int r0 = 0; r0 < 16; r0 += kGatherBatch) {
+      double va[kGatherBatch], vb[kGatherBatch];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t = op_apply(step_op, t, v[i]);
+      for (int r = 0; r < kGatherBatch; ++r) {
+        const int c = hrec * 16 + r0 + r;
+        const int cc = c < cl.size ? c : 0;
+        const auto w4 = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, ((cc * kRec + wave * 64 + 2 * pr) * static_cast<int>(sizeof(double))), 0, 16 /* sc1 */);
+        va[r] = c < cl.size ? __hiloint2double(static_cast<int>(w4[1]), static_cast<int>(w4[0])) : op_identity(step_op);
+        vb[r] = c < cl.size ? __hiloint2double(static_cast<int>(w4[3]), static_cast<int>(w4[2])) : op_identity(step_op);
+      }
+#pragma unroll
+      for (int r = 0; r < kGatherBatch; ++r) {
+        ta = op_apply(step_op, ta, va[r]);
+        tb = op_apply(step_op, tb, vb[r]);
+      }
     }
-    s.red[wave * 64 + lane] = t;
+    {
+      const auto la = __builtin_amdgcn_permlane32_swap(__double2loint(ta), __double2loint(ta), false, false);
+      const auto ha = __builtin_amdgcn_permlane32_swap(__double2hiint(ta), __double2hiint(ta), false, false);
+      const auto lb = __builtin_amdgcn_permlane32_swap(__double2loint(tb), __double2loint(tb), false, false);
+      const auto hb = __builtin_amdgcn_permlane32_swap(__double2hiint(tb), __double2hiint(tb), false, false);
+      ta = op_apply(step_op, __hiloint2double(ha[0], la[0]), __hiloint2double(ha[1], la[1]));
+      tb = op_apply(step_op, __hiloint2double(hb[0], lb[0]), __hiloint2double(hb[1], lb[1]));
+    }
+    if (lane < 32) {
+      s.red[wave * 64 + 2 * pr] = ta;
+      s.red[wave * 64 + 2 * pr + 1] = tb;
+    }
   }
   if (NS > 0 && wave == kWaves - 1) {
 #pragma unroll
@@ -2260,29 +2277,17 @@ bool all_finite(const double* p, int64_t n) {
   return true;
 }
 
-// Clustered launches (a few large problems): workgroups per problem.  Two obstacles per wave of
-// the 512-thread form (16 per workgroup), at most kClusterMax workgroups per problem
+// Clustered launches (a few large problems): workgroups per problem.  One obstacle per wave of
+// the 512-thread form at the most (8 per workgroup), at most kClusterMax workgroups per problem
 // and never more workgroups in all than CUs.  Problems with fewer than kClusterMinObstacles
 // obstacles (≤ 8 rows per thread on one workgroup) stay on one workgroup: the exchanges
 // (~3 per interior-point iteration) would cost more than the sweeps they split (constants
 // kCluster* with the exchange layout above).
-// the most workgroups a problem of this batch may use (1: not eligible for the clustered form)
-int cluster_limit(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
-  if (n_problems < 1 || n_problems > kClusterMaxProblems || n_obstacles < kClusterMinObstacles) return 1;
-  int64_t c = n_obstacles < kClusterMax ? n_obstacles : kClusterMax;
-  c = c < cus / n_problems ? c : cus / n_problems;
-  return c < 2 ? 1 : static_cast<int>(c);
-}
-
-// the workgroups a launch uses: kClusterObstaclesPerGroup obstacles each, or the
-// DRCVAR_MPC_CLUSTER=<c> override (A/B runs; 1 = the one-workgroup form), within the limit
 int cluster_size(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
-  const int lim = cluster_limit(n_problems, n_obstacles, cus);
-  if (lim == 1) return 1;
+  if (n_problems < 1 || n_problems > kClusterMaxProblems || n_obstacles < kClusterMinObstacles) return 1;
   int64_t c = (n_obstacles + kClusterObstaclesPerGroup - 1) / kClusterObstaclesPerGroup;
-  const char* e = std::getenv("DRCVAR_MPC_CLUSTER");
-  if (e && *e) c = std::atoi(e);
-  c = c < lim ? c : lim;
+  c = c < kClusterMax ? c : kClusterMax;
+  c = c < cus / n_problems ? c : cus / n_problems;
   return c < 2 ? 1 : static_cast<int>(c);
 }
 
@@ -2290,6 +2295,14 @@ int cluster_size(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
 __global__ void zero_counters_kernel(double* ws, int n_problems) {
   for (int b = threadIdx.x; b < n_problems; b += blockDim.x)
     __hip_atomic_store((gu64*)(ws + b * kCtrlDoubles), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// DRCVAR_MPC_CLUSTER=<c> caps the workgroups per problem (1: the one-workgroup form); A/B runs
+int cluster_cap() {
+  const char* e = std::getenv("DRCVAR_MPC_CLUSTER");
+  if (!e || !*e) return kClusterMax;
+  const int v = std::atoi(e);
+  return v < 1 ? 1 : v;
 }
 
 int device_cus() {
@@ -2487,7 +2500,7 @@ int drcvar_mpc_model_init(const double* A, const double* B, const double* C, con
 int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_problems,
                                      int64_t n_obstacles) {
   if (!model || n_problems < 0 || n_obstacles < 0) return -1;
-  const int c = cluster_limit(n_problems, n_obstacles, kClusterCUs);  // room for any cluster size
+  const int c = cluster_size(n_problems, n_obstacles, kClusterCUs);
   if (c == 1) return n_problems * (kRowArrays * n_obstacles * kStepPad + kBestPad);
   // clustered: the counters first, then per problem the rows, a best iterate per workgroup and
   // the two exchange buffers
@@ -2498,11 +2511,14 @@ int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_pr
 int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,
                                  int64_t n_obstacles) {
   if (!model || n_problems < 0 || n_obstacles < 0) return -1;
-  if (cluster_limit(n_problems, n_obstacles, kClusterCUs) == 1) return 1;
+  const int c_ws = cluster_size(n_problems, n_obstacles, kClusterCUs);
+  if (c_ws == 1) return 1;
   const int cus = device_cus();
-  const int c = cluster_size(n_problems, n_obstacles, cus > 0 ? cus : 1);
-  const int c_ws = cluster_limit(n_problems, n_obstacles, kClusterCUs);  // what the workspace holds
-  return c < c_ws ? c : c_ws;
+  int c = cluster_size(n_problems, n_obstacles, cus > 0 ? cus : 1);
+  c = c < c_ws ? c : c_ws;
+  const int cap = cluster_cap();
+  c = c < cap ? c : cap;
+  return c < 2 ? 1 : c;
 }
 
 int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
@@ -2570,7 +2586,7 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
   args.ws_off = 0;
   args.ws_pp = kRowArrays * n_obstacles * kStepPad + kBestPad;
   args.cl_size = 1;
-  const int c_ws = cluster_limit(n_problems, n_obstacles, kClusterCUs);
+  const int c_ws = cluster_size(n_problems, n_obstacles, kClusterCUs);
   if (c_ws > 1) {  // the workspace is laid out for c_ws; a smaller device or the cap uses fewer
     args.ws_off = kCtrlDoubles * n_problems;
     args.ws_pp = kRowArrays * n_obstacles * kStepPad + static_cast<int64_t>(c_ws) * (kBestPad + 2 * kRec);

@@ -16,7 +16,8 @@ from mpc_bench import problem_batch  # noqa: E402
 NAMES = {0: "setup", 1: "P1 residuals+weights", 2: "affine rhs", 3: "Riccati factor (ipm)",
          4: "Riccati solves (ipm)", 5: "row passes P2-P5", 6: "loop exit", 7: "polish other",
          8: "output", 10: "polish classify+assemble", 11: "polish Riccati factor",
-         12: "polish row passes", 13: "polish solves", 14: "positions (ipm)", 15: "loop top"}
+         12: "polish row passes", 13: "polish solves", 14: "positions (ipm)", 15: "loop top",
+         16: "cluster exchanges"}
 dev = torch.device("cuda", 0)
 lib = _native.lib()
 lib.drcvar_diag_mpc_stamps.argtypes = [ctypes.c_void_p]
@@ -25,11 +26,19 @@ for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
     model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
     x, u, info = mf.filter_batch(model, rec[..., 3:5], rec[..., 7], x0, xr, uf)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (64 * 16))()
+    buf = (ctypes.c_ulonglong * (64 * 20))()
     assert lib.drcvar_diag_mpc_stamps(ctypes.cast(buf, ctypes.c_void_p)) == 64
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(64, 16)[0].astype(np.int64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(64, 20)[0].astype(np.int64)
     tot = sum(st[k] for k in NAMES)
-    print(f"H={H} O={O}: total {tot} cycles ({tot / 100e6 * 1e3:.3f} ms at 100 MHz memtime), "
+    print(f"groups {model.launch_groups(B, O)}")
+    print(f"H={H} O={O}: total {tot} cycles ({tot / 2.4e9 * 1e3:.3f} ms at 2.4 GHz shader clock), "
           f"iterations {st[9]}, polish attempts {info[0, _native.MPC_INFO_POLISH_ATTEMPTS].item():.0f}")
     for k, nm in NAMES.items():
         print(f"  {nm:28s} {st[k]:10d} ({st[k] / tot * 100:5.1f}%)")
+    cb = (ctypes.c_ulonglong * 8)()
+    lib.drcvar_diag_cluster_stamps.argtypes = [ctypes.c_void_p]
+    if st[16] and lib.drcvar_diag_cluster_stamps(ctypes.cast(cb, ctypes.c_void_p)) == 8:
+        cs = np.frombuffer(cb, dtype=np.uint64).astype(np.int64)  # cumulative over every launch so far
+        names = ["partials+barrier", "combine+stores+drain", "barrier", "arrive+poll", "barrier", "gather"]
+        print("  cluster exchange sub-phases (cumulative, workgroup 0):",
+              ", ".join(f"{n} {cs[i] / max(cs[:6].sum(), 1) * 100:.0f}%" for i, n in enumerate(names)))
