@@ -13,12 +13,15 @@ timing starts.  Exactly K steps are timed: by default as replays of a hipGraph o
 G = min(--graph-batch, K) steps plus one graph of the remainder (`--launch eager`: one ctypes
 call per step).
 
-Multi-GPU (one process per GPU, RCCL): the global batch has O*N_gpus obstacles; rank r draws
-only its own C3-sized block (units [r*O*T, (r+1)*O*T)) with the device sampler, and a step is
-its launch + an all_gather_into_tensor of the 64-B records to every rank (the exchange the QP
-hand-off needs, core/mpc_filter.py:116-151) -- weak scaling, identical per-GPU work at every N.
-The north-star strong-scaling form is the `strong_scaling` key, at every N: ONE global C5 batch
-(256 x 50 x 10 000) sharded over the ranks + the all-gather, and the full loop with the QP.
+Multi-GPU (one process per GPU): the metric line keeps BASELINE's C3 config per GPU — the global
+batch has O*N_gpus obstacles, rank r draws only its own C3-sized block (units [r*O*T,
+(r+1)*O*T)) with the device sampler and a step is its launch; units are independent
+(core/halfspaces.py:225-246), so there is no collective in the step (weak scaling, identical
+per-GPU work at every N).  The north-star form is the `strong_scaling` key, at every N: ONE
+global C5 batch (256 x 50 x 10 000) sharded over the ranks, a step = the shard's launch + an RCCL
+all_gather_into_tensor of the 64-B records to every rank (the exchange the QP hand-off needs,
+core/mpc_filter.py:116-151), and the full loop with the QP.  (A C3 step with the all-gather in
+it measures the all-gather: ~4 us of kernel against tens of us of collective latency.)
 
 Prints ONE JSON line on rank 0: value = units of all ranks / max rank time, plus
   roofline        the kernel on this workload: algorithmic bytes per launch / average launch time
@@ -54,8 +57,9 @@ WORKLOADS = {
 }
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 OUT_BYTES = 64     # 8 fp64 per unit
-# what bounds the sampler (profiles/r02/pmc_sampler*.csv): its per-sample fp64/integer VALU work,
-# not the 16-B store -- its "frac" is the HBM-write fraction it reaches all the same
+# what bounds the sampler (profiles/r02/sampler_pmc.json: VALU busy 1.02 of the SIMD cycles, 190 VALU
+# instructions per sample): its per-sample fp64/integer work, not the 16-B store -- its "frac" is
+# the HBM-write fraction it reaches all the same
 SAMPLER_BOUND = "valu"
 
 
@@ -270,14 +274,10 @@ def main():
     ego = synthetic.straight_line_ego(T, dev)
     sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=42, gather_device=gdev)
     assert sb.count == O * T
-    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev)
+    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev, exchange=False)
     stepper.run(args.warmup)                   # untimed warmup (W steps)
     elapsed, ev_s, K = timed(world, lambda: stepper.run(args.steps), dev, stream)
-    if world == 1:
-        kernel_s, ktiming = ev_s / K, "HIP events over the timed region / K (launch gaps included)"
-    else:
-        kernel_s = kernel_only_time(sb, dev, stream, graph_batch=args.graph_batch)
-        ktiming = "HIP events over graph-replayed kernel-only launches (the timed steps also carry the all-gather)"
+    kernel_s, ktiming = ev_s / K, "HIP events over the timed region / K (launch gaps included)"
 
     strong = None
     if not args.no_large and not args.no_strong:
@@ -303,7 +303,7 @@ def main():
                        "samples": N, "units_per_gpu": sb.count, "global_units_per_step": sb.U,
                        "global_batch": f"{O * world} obstacles x {T} steps x {N} samples, obstacles "
                                        f"[{O}r, {O}r + {O}) on rank r",
-                       "parallelism": f"dp{world}" + ("+allgather" if world > 1 else ""),
+                       "parallelism": f"dp{world}",
                        "launch": stepper.describe(),
                        "alpha": params.alpha, "delta": params.delta, "epsilon": params.epsilon},
             "roofline": dict(roofline(sb.algorithmic_bytes, kernel_s, load_traffic(args.workload)),
