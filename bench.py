@@ -366,7 +366,8 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode):
            "value": sb.U * K / elapsed, "unit": "halfspace-constraints/s", "n_gpus": world,
            "steps": K, "ms_per_step": elapsed / K * 1e3, "scaling": "strong",
            "units_global": sb.U, "units_per_rank": sb.per,
-           "parallelism": f"dp{world}" + ("+allgather (RCCL)" if world > 1 else ""),
+           "parallelism": f"dp{world}" + (f"+allgather ({'RCCL' if gdev is None else 'gloo'})"
+                                           if world > 1 else ""),
            "launch": st.describe(),
            "rank0_kernel_ms": kernel_s * 1e3,
            "rank0_kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK}

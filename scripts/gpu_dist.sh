@@ -1,17 +1,23 @@
 #!/usr/bin/env bash
-# Rehearse the multi-rank bench path on a one-GPU box: gloo, 2 and 4 ranks sharing cuda:0.
+# Rehearse the multi-rank bench path on a one-GPU box: gloo, ranks sharing cuda:0.  2 ranks: the
+# metric line (each rank its own C3 block) and the strong_scaling line (the global C5 batch
+# sharded over the ranks + the all-gather + the full MPC loop); 4 ranks: the metric line.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for n in 2 4; do
-  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 400 --warmup 50 --dist-backend gloo --no-large > gpurun_out/dist_$n.log 2>&1 || { tail -30 gpurun_out/dist_$n.log; exit 2; }
-  grep '^{' gpurun_out/dist_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print($n, d['value'], d['ms_per_step'], d['config']['parallelism'], d['n_gpus'])"
-  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --steps 100 --warmup 10 --dist-backend gloo --no-large --gather > gpurun_out/dist_gather_$n.log 2>&1 || { tail -30 gpurun_out/dist_gather_$n.log; exit 3; }
-  grep '^{' gpurun_out/dist_gather_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print($n, 'gather', d['value'], d['ms_per_step'], d['config']['parallelism'])"
-done
-# full MPC loop (config 5 shape reduced to N=1000 for the rehearsal), 1 and 2 ranks
-timeout -k 10 600 python bench.py --full-loop --workload c5 --steps 10 --warmup 2 > gpurun_out/full_1.log 2>&1 || { tail -20 gpurun_out/full_1.log; exit 4; }
-grep '^{' gpurun_out/full_1.log
-timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29710 bench.py --gpus 2 --full-loop --workload c5 --steps 10 --warmup 2 --dist-backend gloo > gpurun_out/full_2.log 2>&1 || { tail -20 gpurun_out/full_2.log; exit 5; }
-grep '^{' gpurun_out/full_2.log
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29502 bench.py --gpus 2 --steps 400 --warmup 50 --dist-backend gloo --no-cpu-baseline \
+  > gpurun_out/dist_2.log 2>&1 || { tail -30 gpurun_out/dist_2.log; exit 2; }
+grep '^{' gpurun_out/dist_2.log | python3 -c "
+import json, sys
+d = json.loads(sys.stdin.read()); s = d['strong_scaling']
+print(2, d['value'], d['ms_per_step'], d['config']['parallelism'], d['n_gpus'])
+print(2, 'strong', s['value'], s['ms_per_step'], s['parallelism'], s['units_per_rank'], s.get('full_loop'))"
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+  --master-port 29504 bench.py --gpus 4 --steps 400 --warmup 50 --dist-backend gloo --no-large \
+  > gpurun_out/dist_4.log 2>&1 || { tail -30 gpurun_out/dist_4.log; exit 3; }
+grep '^{' gpurun_out/dist_4.log | python3 -c "
+import json, sys
+d = json.loads(sys.stdin.read())
+print(4, d['value'], d['ms_per_step'], d['config']['parallelism'], d['n_gpus'])"
