@@ -760,12 +760,18 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 #endif
 
   // ---- 1. load + moments ----------------------------------------------------------------
-  // Branch-free: idle slots of the last row re-load sample n-1 and contribute zeros.
+  // Branch-free: idle slots of the last row re-load sample n-1 and contribute zeros.  Offsets:
+  // one 64-bit product for the thread's first sample, then a uniform step per row (the clamp is a
+  // select, not a product per sample: the per-sample quarter-rate multiplies sat before the
+  // loads were issued).
   double x[P], y[P];
+  const int64_t off0 = static_cast<int64_t>(tid) * s_samp;
+  const int64_t row_step = static_cast<int64_t>(BLOCK) * s_samp;
+  const int64_t off_last = static_cast<int64_t>(n - 1) * s_samp;
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const int i = tid + j * BLOCK;
-    const int64_t off = static_cast<int64_t>(i < n ? i : n - 1) * s_samp;
+    const int64_t off = i < n ? off0 + j * row_step : off_last;
     if constexpr (LOAD == kLoadNt) {  // streamed once: keep it out of L2 / MALL
       const dbl2 v = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(base + off));
       x[j] = v.x;
