@@ -1137,6 +1137,10 @@ constexpr int kClusterMaxProblems = 8;
 constexpr int kClusterMinObstacles = 64;
 constexpr int kClusterObstaclesPerGroup = 16;  // C5: 16 workgroups (8..32 measured within 4 %)
 constexpr int kClusterMax = 32;
+#ifndef DRCVAR_CLUSTER_BLOCK
+#define DRCVAR_CLUSTER_BLOCK 512
+#endif
+constexpr int kClusterBlock = DRCVAR_CLUSTER_BLOCK;  // threads per workgroup of the clustered form
 constexpr int kClusterCUs = 256;  // workspace sizing; launches use the device's own CU count
 constexpr int kRec = 512;                        // doubles per exchange record
 constexpr int kRecScalars = kPerStepQ * 64;      // [kPerStepQ][64] per-step sums, then scalars
@@ -1181,7 +1185,7 @@ struct Cluster {
 template <int kWaves, int Q, int NS>
 __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* acc, int step_op,
                                        double* sv, const int* ops) {
-  static_assert(Q < kWaves && NS <= 4, "exchange layout");
+  static_assert(Q <= kPerStepQ && NS <= 4, "exchange layout");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* cx = cl.cx;
 #ifdef DRCVAR_MPC_STAMPS
@@ -1201,10 +1205,10 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   // last wave the scalars; every storing wave drains its stores before the barrier behind which
   // one lane signals the arrival for all of them
   double* rec = cl.xbuf + half + static_cast<int64_t>(cl.id) * kRec;
-  if (wave < Q) {
-    double t = s.red[wave * 64 + lane];
-    for (int w = 1; w < kWaves; ++w) t = op_apply(step_op, t, s.red[(w * kPerStepQ + wave) * 64 + lane]);
-    store_wt(rec + wave * 64 + lane, t);
+  for (int q = wave; q < Q; q += kWaves) {
+    double t = s.red[q * 64 + lane];
+    for (int w = 1; w < kWaves; ++w) t = op_apply(step_op, t, s.red[(w * kPerStepQ + q) * 64 + lane]);
+    store_wt(rec + q * 64 + lane, t);
   }
   if (NS > 0 && wave == kWaves - 1) {
 #pragma unroll
@@ -1253,18 +1257,18 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   // last wave gathers the scalars (lane = record).  (16-B loads of step pairs, two halves of the
   // records per wave, measured slower: the extra live registers spilled.)
   const double* base = cl.xbuf + half;
-  if (wave < Q) {
+  for (int q = wave; q < Q; q += kWaves) {
     double v[8];
     double t = op_identity(step_op);
     for (int c0 = 0; c0 < cl.size; c0 += 8) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        v[i] = c0 + i < cl.size ? load_wt(base + static_cast<int64_t>(c0 + i) * kRec + wave * 64 + lane)
+        v[i] = c0 + i < cl.size ? load_wt(base + static_cast<int64_t>(c0 + i) * kRec + q * 64 + lane)
                                 : op_identity(step_op);
 #pragma unroll
       for (int i = 0; i < 8; ++i) t = op_apply(step_op, t, v[i]);
     }
-    s.red[wave * 64 + lane] = t;
+    s.red[q * 64 + lane] = t;
   }
   if (NS > 0 && wave == kWaves - 1) {
 #pragma unroll
@@ -1312,7 +1316,7 @@ constexpr int kSweep = 1;
 // CL: clustered form — a.cl_size workgroups per problem (grid = problems x cl_size), each
 // sweeping the obstacles [o_lo, o_hi) and exchanging row sums (cluster_combine).
 template <int NU, int NX, int BLK, int HMX, bool CL = false>
-__global__ __launch_bounds__(BLK, 2) void mpc_ipm_kernel(MpcArgs a) {
+__global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kernel(MpcArgs a) {
   constexpr int kBlock = BLK;
   constexpr int kWaves = BLK / 64;
   static_assert(kWaves <= kMaxWaves, "LDS plan sized for kMaxWaves");
@@ -2337,8 +2341,8 @@ int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
   const bool few = n_problems <= kFewProblems;
   const bool short_h = args.H <= kShortHorizon;
   if (args.cl_size > 1)
-    return args.nx <= 4 ? launch<NU, 4, 512, DRCVAR_MPC_MAX_HORIZON, true>(args, n_problems, stream)
-                        : launch<NU, 8, 512, DRCVAR_MPC_MAX_HORIZON, true>(args, n_problems, stream);
+    return args.nx <= 4 ? launch<NU, 4, kClusterBlock, DRCVAR_MPC_MAX_HORIZON, true>(args, n_problems, stream)
+                        : launch<NU, 8, kClusterBlock, DRCVAR_MPC_MAX_HORIZON, true>(args, n_problems, stream);
   if (args.nx <= 4)
     return few ? launch<NU, 4, 512>(args, n_problems, stream)
                : short_h ? launch<NU, 4, 128, kShortHorizon>(args, n_problems, stream)
