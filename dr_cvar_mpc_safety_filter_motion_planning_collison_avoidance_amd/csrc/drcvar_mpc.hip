@@ -157,7 +157,7 @@ struct Lds {
   double* Kg;     // [H][NU][NX] feedback gains Re^-1 B'PA
   double* Ri;     // [H][NU][NU] Re^-1
   double* SM;     // [H][NX][NX] solve maps F_k = A' - Kg_k' B' (NX <= 4)
-  double* SV;     // [H][NX] solve recurrences' sources and states (NX <= 4)
+  double* SV;     // [H + 1][NX] solve recurrences' sources and states (NX <= 4)
   double* u;      // [n] inputs (the iterate)
   double* dua;    // [n] affine direction
   double* du;     // [n] corrector direction
@@ -205,8 +205,8 @@ struct LdsPlan {
   static constexpr int Kg = U + kMx * kMu;
   static constexpr int Ri = Kg + HM * NU * NX;
   static constexpr int SM = Ri + HM * NU * NU;                   // solve: [HM][NX][NX] maps
-  static constexpr int SV = SM + (NX <= 4 ? HM * NX * NX : 0);   // solve: [HM][NX] vectors
-  static constexpr int u = SV + (NX <= 4 ? HM * NX : 0);
+  static constexpr int SV = SM + (NX <= 4 ? HM * NX * NX : 0);   // solve: [HM + 1][NX] vectors
+  static constexpr int u = SV + (NX <= 4 ? (HM + 1) * NX : 0);
   static constexpr int dua = u + NMAX;
   static constexpr int du = dua + NMAX;
   static constexpr int rdu = du + NMAX;
@@ -891,10 +891,12 @@ __device__ __forceinline__ void load_fwd(StepData& d, const double* M, const dou
   d.w = G[kk * 4 + i];
 }
 
+// With pos: also the positions the solution produces, pos[2k+i] = c[2k+i] + (C x_{k+1})_i (c may
+// be null: 0) — read off the forward pass's states instead of a separate Mp convolution.
 template <int NU, int kBlock>
-__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x) {
+__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c) {
   const int t = threadIdx.x;
-  double* W = s.SV;   // [H][4]: Kg_k' b_k, then p_k (backward pass), then x_k (forward pass)
+  double* W = s.SV;   // [H + 1][4]: Kg_k' b_k, then p_k (backward pass), then x_k (forward pass)
   double* G = s.red;  // [H][4]: B kff_k
   const double* M = s.SM;
   for (int e = t; e < H * 4; e += kBlock) {
@@ -973,6 +975,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x) {
         load_fwd(d[q], M, G, k + q + 4, i, H);
       }
     }
+    if (keeper && Hp == H) W[H * 4 + i] = xs;  // x_H (with padding the loop stored it)
   }
   __syncthreads();
   // du_k = kff_k - Kg_k x_k
@@ -983,16 +986,31 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x) {
     for (int m = 0; m < 4; ++m) acc -= s.Kg[(k * NU + u) * 4 + m] * W[k * 4 + m];
     x[e] = acc;
   }
+  if (pos) {  // p_k = c_k + C x_{k+1}
+    for (int e = t; e < 2 * H; e += kBlock) {
+      const int k = e >> 1, i = e & 1;
+      double acc = c ? c[e] : 0.0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc += s.Cm[i * kMx + m] * W[(k + 1) * 4 + m];
+      pos[e] = acc;
+    }
+  }
   __syncthreads();
 }
 
-// K x = b: the DPP recurrences for NX <= 4, the wave-serial recursion otherwise
+// K x = b: the DPP recurrences for NX <= 4, the wave-serial recursion otherwise.  With pos: the
+// positions of the solution as well, pos = c + Gp x (c may be null).  Ends with a barrier.
 template <int NU, int NX, int kBlock, int HMX>
-__device__ inline void newton_solve(const Lds& s, int H, double* x) {
+__device__ inline void newton_solve(const Lds& s, int H, double* x, double* pos = nullptr,
+                                    const double* c = nullptr) {
   if constexpr (NX <= 4) {
-    riccati_solve_dpp<NU, kBlock>(s, H, x);
+    riccati_solve_dpp<NU, kBlock>(s, H, x, pos, c);
   } else {
     riccati_solve<NU, NX>(s, H, x);
+    if (pos) {
+      positions<NU, kBlock>(s, x, pos, c, H);
+      __syncthreads();
+    }
   }
 }
 
@@ -1597,11 +1615,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       break;
     }
     MPC_PHASE(3);
-    newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua);
+    newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa);  // direction and its positions
     MPC_PHASE(4);
-    positions<NU, kBlock>(s, s.dua, s.dpa, nullptr, H);
-    __syncthreads();
-    MPC_PHASE(14);
 
     // ---- P2+P3: affine step length, affine gap, corrector rhs — one sweep of the rows ----
     // The corrector rhs sums do not depend on the affine step a_aff, and a row's affine gap
@@ -1721,11 +1736,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     const double sigma_mu = s.sc[63];
     MPC_PHASE(5);
-    newton_solve<NU, NX, kBlock, HMX>(s, H, s.du);
+    newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.dp);
     MPC_PHASE(4);
-    positions<NU, kBlock>(s, s.du, s.dp, nullptr, H);
-    __syncthreads();
-    MPC_PHASE(14);
 
     // ---- P4: corrector step length ----
     amax = kHuge;
@@ -1803,11 +1815,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     __syncthreads();  // positions of the box loop read s.u; update it only after every reader
     for (int j = tid; j < n; j += kBlock) s.u[j] += alpha * s.du[j];
+    for (int t = tid; t < 2 * H; t += kBlock) s.p[t] += alpha * s.dp[t];
     __syncthreads();
     MPC_PHASE(5);
-    positions<NU, kBlock>(s, s.u, s.p, s.c, H);  // of the updated iterate (next iteration's P1)
-    __syncthreads();
-    MPC_PHASE(14);
     // fused pass: each halfspace row is updated (P5) and enters the next iteration's P1 sums
     p1_clear();
     if (lane < K) {
@@ -1979,10 +1989,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
         __syncthreads();
         MPC_PHASE(12);
-        newton_solve<NU, NX, kBlock, HMX>(s, H, s.du);
+        newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.p, s.c);  // u and its positions
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
-        __syncthreads();
-        positions<NU, kBlock>(s, s.u, s.p, s.c, H);
         __syncthreads();
         MPC_PHASE(13);
         // multiplier updates nu += rho * (E u - e); eres = |E u - e|_inf

@@ -1,0 +1,34 @@
+"""Dump scripts/mpc_bench.py's QP problems (halfspace rows from the engine on the device) and the
+kernel's answers to gpurun_out/qp_problems.npz, for CPU experiments with the interior-point method
+(scripts/micro/ipm_lab.py)."""
+import os
+import sys
+
+sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.join(os.getcwd(), "scripts"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native  # noqa: E402
+from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf  # noqa: E402
+from mpc_bench import problem_batch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+out = {}
+for shape in ["50,256,1,0", "50,256,1,1", "50,256,1,2", "50,256,3,5", "30,3,4,0", "20,10,3,0",
+              "20,100,1,0", "30,64,2,0"]:
+    H, O, B, seed = (int(v) for v in shape.split(","))
+    model, rec, x0, xr, uf = problem_batch(H, O, B, dev, seed=seed)
+    h, g = rec[..., 3:5], rec[..., 7]
+    x, u, info = mf.filter_batch(model, h, g, x0, xr, uf)
+    torch.cuda.synchronize()
+    key = f"H{H}_O{O}_B{B}_s{seed}"
+    out[key + "_h"] = h.cpu().numpy()
+    out[key + "_g"] = g.cpu().numpy()
+    out[key + "_x0"] = x0.cpu().numpy()
+    out[key + "_xr"] = xr.cpu().numpy()
+    out[key + "_u"] = u.cpu().numpy()
+    out[key + "_info"] = info.cpu().numpy()
+    print(key, "iters", info[:, _native.MPC_INFO_ITERATIONS].cpu().numpy(), flush=True)
+os.makedirs("gpurun_out", exist_ok=True)
+np.savez_compressed("gpurun_out/qp_problems.npz", **out)
