@@ -51,8 +51,11 @@ constexpr int kMaxWaves = 8;
 constexpr int kFewProblems = 128;  // at most this many problems per launch: 512-thread form
 constexpr int kShortHorizon = 32;  // horizon capacity of the 128-thread (many problems) form
 constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
-constexpr int kRowArrays = 8; // h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
-constexpr int kBestPad = 128; // best iterate u (n <= DRCVAR_MPC_MAX_DECISION)
+// h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s, then s and w_hs saved across a failed polish
+constexpr int kRowArrays = 10;
+// per workgroup: the best iterate u (n <= DRCVAR_MPC_MAX_DECISION, padded to 128), then the bound
+// states saved across a failed polish (bx [4 n], px [8 H]: <= 992)
+constexpr int kBestPad = 128 + 1024;
 constexpr int kRowStride = kRowArrays * kStepPad;  // one obstacle's block of the workspace
 constexpr double kSlackLin = 50.0;    // core/mpc_filter.py:143
 constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:144
@@ -64,6 +67,9 @@ constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
 constexpr double kPolishDualTol = 1e-7;
+constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
+constexpr int kResumeIters = 8;         // interior-point iterations after a failed polish
+constexpr double kResumeTol = 1e-3;     // ... towards tol * kResumeTol
 constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
 
 #ifdef DRCVAR_MPC_STAMPS
@@ -1408,7 +1414,13 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   }
   __syncthreads();
 
-  // start: u = 0, s = 0, w = max(d - Gz, 1), lambda = 1 except the slack rows' (below)
+  // start: u = 0, s = 0, w = max(d - Gz, 1), lambda = 1 except the slack rows' (below).  With
+  // many obstacles the halfspace rows start at lambda = 8 and their slack rows at w = 3: counted
+  // on the CPU restatement (scripts/micro/ipm_lab.py, 58 device-dumped problems) that takes the
+  // 256-obstacle C5 hand-off from 17 to 14.5 iterations and O = 64..128 by ~1; with a few
+  // obstacles (main.py: 3) the unit start stays ahead, so the switch is by obstacle count.
+  const bool many_rows = O >= kManyRowsObstacles;
+  const double lA0 = many_rows ? 8.0 : 1.0, wB0 = many_rows ? 3.0 : 1.0;
   double gmax = 0.0;
   if (lane < K) {
     const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
@@ -1422,8 +1434,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       rows.g[r] = g;
       rows.s[r] = 0.0;
       rows.wA[r] = fmax(-(h0 * c0 + h1 * c1 + g), 1.0);
-      rows.lA[r] = 1.0;
-      rows.wB[r] = 1.0;
+      rows.lA[r] = lA0;
+      rows.wB[r] = wB0;
       // the dual of s >= 0 ends at kSlackLin - lambda_hs in [0, kSlackLin] (kSlackLin where the
       // halfspace is slack, the common case): start midway, not at 1 (main.py QP 9 -> 6
       // iterations, C5 18 -> 16; 10, 25 and 50 measured, 25 best across the shapes)
@@ -1497,7 +1509,27 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     rpm_rows = fmax(rpm_rows, fmax(fabs(l.rpA), fabs(l.rpB)));
     rdm_rows = fmax(rdm_rows, fabs(l.rds));
   };
-  // positions of the starting iterate and its P1 row pass
+  // Rounds: the interior-point method to tol, then the polish.  When the polish fails on a problem
+  // that met tol (degenerate active sets: more binding rows than freedom), the interior-point
+  // state the polish overwrote is restored and the method continues for up to kResumeIters
+  // iterations towards tol * kResumeTol, then polishes once more; its iterate stands if that
+  // polish fails too.  (Degenerate problems converge in u only like sqrt(mu): at merit 1e-8 the
+  // answer can be 1e-5 off.)  Every decision is uniform, so a cluster takes the rounds together.
+  double tol_r = a.tol;
+  int it_end = a.max_iter;
+  int polish_attempts = 0;
+  bool polished = false;
+  // saved across a failed polish: the rows' s and w_hs (fields 8, 9 of every obstacle block) and
+  // the bound states bx [4 n], px [8 H] (behind the best iterate)
+#define SAVED_S (ws + 8 * kStepPad)
+#define SAVED_W (ws + 9 * kStepPad)
+#define SAVED_B (ws + kRowArrays * pitch + static_cast<int64_t>(cid) * kBestPad + 128)
+  it = 1;
+  // one round: P1 of the current iterate, the interior-point loop, the polish; true when a resume
+  // round should follow.  Inlined at both call sites (a loop around it, or an out-of-line
+  // function, made the compiler spill inside the interior-point loop: C5 QP +5 % / +40 %).
+  auto ipm_round = [&](const int round) __attribute__((always_inline)) -> bool {
+  // positions of the starting (or restored) iterate and its P1 row pass
   positions<NU, kBlock>(s, s.u, s.p, s.c, H);
   __syncthreads();
   p1_clear();
@@ -1507,7 +1539,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       p1_row(q, p0, p1);
     ROW_SWEEP_END
   }
-  for (it = 1; it <= a.max_iter; ++it) {
+  for (; it <= it_end; ++it) {
     MPC_PHASE(15);
 
     // ---- P1: residuals, weights, per-step S / v / affine rhs (row sums already taken) ----
@@ -1586,7 +1618,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         break;
       }
       const double merit = fmax(fmax(rp / scale_d, rd / scale_q), mu);
-      if (merit <= a.tol) {
+      if (merit <= tol_r) {
         status = DRCVAR_MPC_STATUS_OPTIMAL;
         best_merit = merit;
         break;
@@ -1841,12 +1873,13 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     MPC_PHASE(5);
   }
-  if (it > a.max_iter) it = a.max_iter;
+  if (it > it_end) it = it_end;
   __syncthreads();
   MPC_PHASE(6);
   if (status != DRCVAR_MPC_STATUS_OPTIMAL && best_merit <= 1e3 * a.tol) {
-    // stalled close to the optimum: return the best iterate, its slacks re-optimised below
-    status = DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
+    // stalled close to the optimum (or a resumed round short of its tighter tolerance): return
+    // the best iterate, its slacks re-optimised below
+    status = best_merit <= a.tol ? DRCVAR_MPC_STATUS_OPTIMAL : DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
     for (int j = tid; j < n; j += kBlock) s.u[j] = best_u[j];
   }
 
@@ -1856,9 +1889,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // reuse the Hessian assembly, the Cholesky and the triangular solves), and rows whose sign
   // conditions fail are moved (primal-dual active-set step), up to kPolishAttempts times.  On
   // success the answer is exact to roundoff; otherwise the interior-point answer stands.
-  int polish_attempts = 0;
-  bool polished = false;
-  if (a.polish && best_merit <= kPolishMerit && true) {
+  const bool tried = a.polish && best_merit <= kPolishMerit;
+  if (tried) {
     for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];  // the answer if polishing fails
     // classify: flag 0 = halfspace not binding (s = 0), 1 = slack positive (s = h.p + g > 0),
     // 2 = binding with s = 0 (equality, multiplier nu in [0, 50]); rows.s <- nu, rows.wA <- flag
@@ -1867,6 +1899,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
         const bool actA = rows.lA[r] > rows.wA[r], actB = rows.lB[r] > rows.wB[r];
         const double flag = actA ? (actB ? 2.0 : 1.0) : 0.0;
+        SAVED_S[r] = rows.s[r];
+        SAVED_W[r] = rows.wA[r];
         rows.s[r] = flag == 2.0 ? rows.lA[r] : 0.0;
         rows.wA[r] = flag;
       }
@@ -1876,6 +1910,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       for (int j = tid; j < n; j += kBlock) {
         const PairState q = box_state(s, n, j);
         const bool up = q.lu > q.wu, lo = q.ll > q.wl;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) SAVED_B[k * n + j] = s.bx[k * n + j];
         s.bx[j] = up;
         s.bx[n + j] = up ? q.lu : 0.0;
         s.bx[2 * n + j] = lo;
@@ -1886,6 +1922,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       for (int t = tid; t < 2 * H; t += kBlock) {
         const PairState q = pos_state(s, H, t);
         const bool up = q.lu > q.wu, lo = q.ll > q.wl;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) SAVED_B[4 * n + k * 2 * H + t] = s.px[k * 2 * H + t];
         s.px[t] = up;
         s.px[2 * H + t] = up ? q.lu : 0.0;
         s.px[4 * H + t] = lo;
@@ -2158,6 +2196,30 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     __syncthreads();
   }
+  bool resume = round == 0 && tried && !polished && status == DRCVAR_MPC_STATUS_OPTIMAL && it < a.max_iter;
+  if constexpr (CL) resume = resume && !cl.aborted;
+  if (!resume) return false;
+  // restore what the polish overwrote (u is back already): the rows' s / w_hs and the bound states
+  if (lane < K) {
+    for (int o = o_lo + wave; o < o_hi; o += kWaves) {
+      const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
+      rows.s[r] = SAVED_S[r];
+      rows.wA[r] = SAVED_W[r];
+    }
+  }
+  for (int j = tid; j < n; j += kBlock)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s.bx[k * n + j] = SAVED_B[k * n + j];
+  for (int t = tid; t < 2 * H; t += kBlock)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s.px[k * 2 * H + t] = SAVED_B[4 * n + k * 2 * H + t];
+  __syncthreads();
+  status = DRCVAR_MPC_STATUS_MAX_ITER;
+  tol_r = a.tol * kResumeTol;
+  it_end = it + kResumeIters < a.max_iter ? it + kResumeIters : a.max_iter;
+  return true;
+  };  // ipm_round
+  if (ipm_round(0)) ipm_round(1);
 
   MPC_PHASE(7);
   // ------------------------------- output -------------------------------

@@ -15,8 +15,14 @@ from mpc_bench import problem_batch  # noqa: E402
 
 dev = torch.device("cuda", 0)
 out = {}
-for shape in ["50,256,1,0", "50,256,1,1", "50,256,1,2", "50,256,3,5", "30,3,4,0", "20,10,3,0",
-              "20,100,1,0", "30,64,2,0"]:
+SHAPES = ["50,256,1,0", "50,256,1,1", "50,256,1,2", "50,256,3,5", "30,3,4,0", "20,10,3,0",
+          "20,100,1,0", "30,64,2,0"]
+if len(sys.argv) > 1 and sys.argv[1] == "wide":  # a wider set for validation: more seeds per shape
+    SHAPES = ([f"50,256,2,{s}" for s in range(10, 20, 2)] + [f"30,3,8,{s}" for s in (20, 30)] +
+              [f"20,100,2,{s}" for s in (40, 42, 44)] + [f"30,64,2,{s}" for s in (50, 52, 54)] +
+              [f"40,128,2,{s}" for s in (60, 62)] + [f"20,10,4,{s}" for s in (70, 71)])
+OUT = "gpurun_out/qp_problems_wide.npz" if SHAPES[0] != "50,256,1,0" else "gpurun_out/qp_problems.npz"
+for shape in SHAPES:
     H, O, B, seed = (int(v) for v in shape.split(","))
     model, rec, x0, xr, uf = problem_batch(H, O, B, dev, seed=seed)
     h, g = rec[..., 3:5], rec[..., 7]
@@ -31,4 +37,4 @@ for shape in ["50,256,1,0", "50,256,1,1", "50,256,1,2", "50,256,3,5", "30,3,4,0"
     out[key + "_info"] = info.cpu().numpy()
     print(key, "iters", info[:, _native.MPC_INFO_ITERATIONS].cpu().numpy(), flush=True)
 os.makedirs("gpurun_out", exist_ok=True)
-np.savez_compressed("gpurun_out/qp_problems.npz", **out)
+np.savez_compressed(OUT, **out)

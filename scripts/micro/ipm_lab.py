@@ -39,7 +39,7 @@ def model(H, dt=0.2):
                 pmin=np.full(2 * H, -10.0), pmax=np.full(2 * H, 10.0))
 
 
-START = dict(wA_floor=1.0, lA=1.0, wB=1.0, lB=0.5 * SLACK_LIN, box_l=1.0)
+START = dict(wA_floor=1.0, lA=1.0, wB=1.0, lB=0.5 * SLACK_LIN, box_l=1.0, lA_many=8.0, wB_many=3.0)
 
 
 def solve(md, h, g, x0, xr, variant="base", tol=1e-8, max_iter=60, trace=False):
@@ -61,8 +61,9 @@ def solve(md, h, g, x0, xr, variant="base", tol=1e-8, max_iter=60, trace=False):
     u = np.zeros(n)
     s = np.zeros((O, H))
     wA = np.maximum(-(hp_of(c) + g), START["wA_floor"])
-    lA = np.full((O, H), START["lA"])
-    wB = np.full((O, H), START["wB"])
+    many = O >= START.get("many", 1e9)  # the kernel's rule: other starting values for many rows
+    lA = np.full((O, H), START["lA_many"] if many else START["lA"])
+    wB = np.full((O, H), START["wB_many"] if many else START["wB"])
     lB = np.full((O, H), START["lB"])
     bl = START["box_l"]
     wUu, lUu = np.maximum(md["umax"], 1.0), np.full(n, bl)

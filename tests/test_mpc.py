@@ -169,7 +169,7 @@ def test_workspace_size():
     A, B, C = double_integrator()
     _, m, _ = model_init(A, B, C, 2 * np.eye(4), np.eye(2), 30, blob=False)
     ws = _native.lib().drcvar_mpc_workspace_doubles(ctypes.byref(m), 3, 10)
-    assert ws == 3 * (8 * 10 * 64 + 128)
+    assert ws == 3 * (10 * 10 * 64 + 1152)
 
 
 def test_filter_argument_validation_host_side():

@@ -17,7 +17,7 @@ import pytest
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
 from test_mpc import MPC_TOL, _oracle, _random_problem, double_integrator, model_init
 
-CTRL, ROWS, BEST, REC = 16, 8 * 64, 128, 512
+CTRL, ROWS, BEST, REC = 16, 10 * 64, 1152, 512
 
 
 @pytest.mark.parametrize("B,O,groups", [(1, 256, 16), (1, 64, 4), (3, 100, 7), (8, 70, 5),
