@@ -526,7 +526,13 @@ def mpc_handoff(dev, samples, ego, params, with_cpu):
           "halfspace_constraints_per_s_full_loop": O * T / (full_ms * 1e-3),
           "qp_status": mf.STATUS_NAMES.get(int(info[_native.MPC_INFO_STATUS])),
           "qp_iterations": int(info[_native.MPC_INFO_ITERATIONS]),
-          "polished": bool(info[_native.MPC_INFO_POLISHED])}
+          "polished": bool(info[_native.MPC_INFO_POLISHED]),
+          "polish_attempts": int(info[_native.MPC_INFO_POLISH_ATTEMPTS])}
+    if os.environ.get("DRCVAR_BENCH_DUMP_QP"):  # diagnostics: the C5 QP's inputs (scripts/micro/ipm_lab.py)
+        np.savez_compressed(os.environ["DRCVAR_BENCH_DUMP_QP"], **{
+            f"H{H}_O{O}_B1_bench_h": h.cpu().numpy(), f"H{H}_O{O}_B1_bench_g": g.cpu().numpy(),
+            f"H{H}_O{O}_B1_bench_x0": x0.cpu().numpy(), f"H{H}_O{O}_B1_bench_xr": xr.cpu().numpy(),
+            f"H{H}_O{O}_B1_bench_u": res["u"].cpu().numpy(), f"H{H}_O{O}_B1_bench_info": res["info"].cpu().numpy()})
     if with_cpu:
         from oracle import mpc_qp
         r = rec.cpu().numpy()

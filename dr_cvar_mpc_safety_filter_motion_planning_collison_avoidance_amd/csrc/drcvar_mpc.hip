@@ -1415,12 +1415,13 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   __syncthreads();
 
   // start: u = 0, s = 0, w = max(d - Gz, 1), lambda = 1 except the slack rows' (below).  With
-  // many obstacles the halfspace rows start at lambda = 8 and their slack rows at w = 3: counted
-  // on the CPU restatement (scripts/micro/ipm_lab.py, 58 device-dumped problems) that takes the
-  // 256-obstacle C5 hand-off from 17 to 14.5 iterations and O = 64..128 by ~1; with a few
-  // obstacles (main.py: 3) the unit start stays ahead, so the switch is by obstacle count.
+  // many obstacles the halfspace rows start at lambda = 5 and their slack rows at w = 1.5: counted
+  // on the CPU restatement (scripts/micro/ipm_lab.py) over three families of device-dumped
+  // problems (72 in all: scripts/mpc_bench.py's, a wider seed set of them, and bench.py's C5-style
+  // hand-offs) that is 7 % fewer iterations in each family and 6-13 % on the 256-obstacle ones;
+  // with a few obstacles (main.py: 3) the unit start stays ahead, so the switch is by obstacle count.
   const bool many_rows = O >= kManyRowsObstacles;
-  const double lA0 = many_rows ? 8.0 : 1.0, wB0 = many_rows ? 3.0 : 1.0;
+  const double lA0 = many_rows ? 5.0 : 1.0, wB0 = many_rows ? 1.5 : 1.0;
   double gmax = 0.0;
   if (lane < K) {
     const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];

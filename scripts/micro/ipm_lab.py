@@ -39,10 +39,11 @@ def model(H, dt=0.2):
                 pmin=np.full(2 * H, -10.0), pmax=np.full(2 * H, 10.0))
 
 
-START = dict(wA_floor=1.0, lA=1.0, wB=1.0, lB=0.5 * SLACK_LIN, box_l=1.0, lA_many=8.0, wB_many=3.0)
+START = dict(wA_floor=1.0, lA=1.0, wB=1.0, lB=0.5 * SLACK_LIN, box_l=1.0, lA_many=5.0, wB_many=1.5, many=64)
 
 
-def solve(md, h, g, x0, xr, variant="base", tol=1e-8, max_iter=60, trace=False):
+def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False):
+    tol = START.get("tol", 1e-8) if tol is None else tol
     """h [O, H, 2], g [O, H].  Returns (u, iterations, merit history)."""
     H, n = md["H"], md["n"]
     Gp = md["Gp"]                                   # [2H, n]: p = c + Gp u
@@ -152,13 +153,13 @@ def solve(md, h, g, x0, xr, variant="base", tol=1e-8, max_iter=60, trace=False):
         a_aff = min(1.0, amax_of(d_a, who))
         gap_aff = sum(((state[k][0] + a_aff * d_a[k][0]) * (state[k][1] + a_aff * d_a[k][1])).sum()
                       for k in state)
-        sigma_mu = (gap_aff / gap) ** 3 * mu
+        sigma_mu = (gap_aff / gap) ** START.get("sig_exp", 3.0) * mu
         rc = {k: -w_ * l_ - d_a[k][0] * d_a[k][1] + sigma_mu for k, (w_, l_) in state.items()}
         du, ds, d = direction(rc)
         amax = amax_of(d)
         if variant == "gondzio":
             du, ds, d, amax = gondzio(direction, amax_of, state, rc, du, ds, d, amax, sigma_mu)
-        alpha = min(1.0, (1.0 - min(1.0 - STEP_FRAC, mu)) * amax)
+        alpha = min(1.0, (1.0 - min(1.0 - START.get("frac", STEP_FRAC), mu)) * amax)
         if variant == "split":   # separate primal (u, s, w) and dual (lambda) step lengths
             ap_ = np.inf
             ad_ = np.inf

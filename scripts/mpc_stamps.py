@@ -21,10 +21,30 @@ NAMES = {0: "setup", 1: "P1 residuals+weights", 2: "affine rhs", 3: "Riccati fac
 dev = torch.device("cuda", 0)
 lib = _native.lib()
 lib.drcvar_diag_mpc_stamps.argtypes = [ctypes.c_void_p]
+def npz_problem(path, key):
+    """A problem saved by scripts/micro/dump_bench_qps.py / dump_qp_problems.py (double integrator)."""
+    z = np.load(path)
+    h, g, x0, xr = (torch.as_tensor(z[f"{key}_{s}"]).to(dev) for s in ("h", "g", "x0", "xr"))
+    H = int(key.split("_")[0][1:])
+    dt = 0.2
+    A = np.block([[np.eye(2), dt * np.eye(2)], [np.zeros((2, 2)), np.eye(2)]])
+    Bm = np.block([[0.5 * dt ** 2 * np.eye(2)], [dt * np.eye(2)]])
+    C = np.block([np.eye(2), np.zeros((2, 2))])
+    model = mf.MPCModel(A, Bm, C, 2 * np.eye(4), np.eye(2), H, (np.full(2, -5.0), np.full(2, 5.0)),
+                        (np.full(2, -10.0), np.full(2, 10.0)), device=dev)
+    return model, h, g, x0, xr, torch.zeros((h.shape[0], H, 2), dtype=torch.float64, device=dev)
+
+
 for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
-    H, O, B = (int(v) for v in shape.split(","))
-    model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
-    x, u, info = mf.filter_batch(model, rec[..., 3:5], rec[..., 7], x0, xr, uf)
+    if shape.startswith("npz:"):  # npz:<path>:<key>
+        _, path, key = shape.split(":")
+        model, h, g, x0, xr, uf = npz_problem(path, key)
+        B, O, H = h.shape[0], h.shape[1], h.shape[2]
+    else:
+        H, O, B = (int(v) for v in shape.split(","))
+        model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
+        h, g = rec[..., 3:5], rec[..., 7]
+    x, u, info = mf.filter_batch(model, h, g, x0, xr, uf)
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (64 * 20))()
     assert lib.drcvar_diag_mpc_stamps(ctypes.cast(buf, ctypes.c_void_p)) == 64
