@@ -145,6 +145,7 @@ struct MpcArgs {
   double* ws;
   int64_t ws_off, ws_pp;  // per-problem region b at ws + ws_off + b * ws_pp
   int cl_size;            // workgroups per problem (clustered form)
+  int force_resume;       // test hook (DRCVAR_MPC_FORCE_RESUME=1): the first polish makes no attempt
   int max_iter;
   double tol;
   int polish;
@@ -1934,6 +1935,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     __syncthreads();
     const double tolf = 1e-9 * scale_d;
     for (int attempt = 0; attempt < kPolishAttempts && !polished; ++attempt) {
+      // test hook; a loop bound computed from it instead (attempts = hook ? 0 : kPolishAttempts)
+      // broke the 4-input kernels' polish (8 % polished) — a codegen effect, not a semantic one
+      if (round == 0 && a.force_resume) break;
       ++polish_attempts;
       // Hessian of the active-set problem: 100 h h' for positive slacks, rho h h' for equalities
       {
@@ -2654,6 +2658,10 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
   args.max_iter = max_iter;
   args.tol = tol;
   args.polish = polish;
+  {  // test hook: every problem that meets tol takes the resume round (tests/test_mpc_cluster.py)
+    const char* fr = std::getenv("DRCVAR_MPC_FORCE_RESUME");
+    args.force_resume = fr && fr[0] == '1';
+  }
 
   (void)hipGetLastError();
   auto st = static_cast<hipStream_t>(stream);

@@ -167,3 +167,27 @@ def test_gpu_cluster_graph_replay(dev, cluster_size):
         torch.cuda.synchronize()
         assert torch.equal(out[0], x_e) and torch.equal(out[1], u_e) and torch.equal(out[2], i_e)
     _check_vs_oracle(probs, x_e.cpu().numpy(), u_e.cpu().numpy(), i_e.cpu().numpy(), "graph")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dyn,H,O,B,tight", [
+    ("double", 50, 256, 1, False),  # the clustered C5 shape
+    ("double", 30, 6, 3, True),     # one workgroup per problem
+    ("generic3", 24, 70, 2, True),  # clustered, three inputs
+])
+def test_gpu_resume_after_failed_polish(dyn, H, O, B, tight, dev, cluster_size, monkeypatch):
+    """DRCVAR_MPC_FORCE_RESUME=1 makes the first polish give up at once, so every problem takes
+    the resume round (csrc/drcvar_mpc.hip, ipm_round): the interior-point state the polish
+    overwrote is restored (the rows' s / w_hs, the bound states, u), the method continues towards
+    tol * 1e-3 and polishes again.  The answer must match the oracle and the normal path."""
+    probs = _batch(dyn, H, O, B, tight, seed=7 * H + O + B)
+    cluster_size(None)
+    x, u, info, _ = _solve(probs, dev)
+    monkeypatch.setenv("DRCVAR_MPC_FORCE_RESUME", "1")
+    x2, u2, info2, _ = _solve(probs, dev)
+    _check_vs_oracle(probs, x2, u2, info2, "resumed")
+    assert np.all(info2[:, _native.MPC_INFO_ITERATIONS] >= info[:, _native.MPC_INFO_ITERATIONS])
+    assert np.all(info2[:, _native.MPC_INFO_POLISH_ATTEMPTS] >= 1)
+    both = (info[:, _native.MPC_INFO_POLISHED] == 1) & (info2[:, _native.MPC_INFO_POLISHED] == 1)
+    np.testing.assert_allclose(u2[both], u[both], atol=MPC_TOL)
+    np.testing.assert_allclose(x2[both], x[both], atol=MPC_TOL)
