@@ -371,9 +371,10 @@ def test_gpu_many_problems_every_form(dyn, H, O, dev):
     fallback; problems polished in both forms agree; sampled problems match the oracle.
 
     Random instances with several tight halfspaces binding at one step are degenerate (more active
-    rows than inputs).  There the active-set polish can fail — then the interior-point answer is
-    returned as OPTIMAL_INACCURATE, within 1e-5 of the oracle — on up to ~15 % of generic1 problems
-    (one input), a few % elsewhere; the bounds below hold that rate."""
+    rows than inputs).  There the first active-set polish often fails; the kernel then resumes the
+    interior-point method towards tol * 1e-3 and polishes again (csrc/drcvar_mpc.hip, ipm_round),
+    which polishes >= 99 % of every set here (scripts/micro/census.py; before the resume round
+    ~10-15 % of the one-input problems ended OPTIMAL_INACCURATE).  The bound below holds that."""
     import torch
     from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
     rng = np.random.default_rng(H * 100 + O)
@@ -405,7 +406,7 @@ def test_gpu_many_problems_every_form(dyn, H, O, dev):
         assert np.all(np.isin(info[:, _native.MPC_INFO_STATUS], ok_status)), info[:, 0]
         assert np.all(info[:, _native.MPC_INFO_USED_FALLBACK] == 0)
         pol = info[:, _native.MPC_INFO_POLISHED] == 1
-        assert pol.mean() >= (0.8 if dyn == "generic1" else 0.95), pol.mean()
+        assert pol.mean() >= 0.97, pol.mean()
         polished.append(pol)
     both = polished[0] & polished[1]
     np.testing.assert_allclose(many[1][both], few[1][both], atol=MPC_TOL)
