@@ -42,7 +42,7 @@ def model(H, dt=0.2):
 START = dict(wA_floor=1.0, lA=1.0, wB=1.0, lB=0.5 * SLACK_LIN, box_l=1.0, lA_many=5.0, wB_many=1.5, many=64)
 
 
-def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False):
+def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False, on_system=None):
     tol = START.get("tol", 1e-8) if tol is None else tol
     """h [O, H, 2], g [O, H].  Returns (u, iterations, merit history)."""
     H, n = md["H"], md["n"]
@@ -110,6 +110,8 @@ def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False):
         for k in range(H):
             Sb[2 * k:2 * k + 2, 2 * k:2 * k + 2] = S[k]
         K = md["H0"] + np.diag(DUu + DUl) + Gp.T @ Sb @ Gp
+        if on_system is not None:  # scripts/micro/riccati_scan_lab.py: the Newton system's LQ data
+            on_system(it, merit, S, DUu + DUl, K)
         L = np.linalg.cholesky(K)
         state = dict(A=(wA, lA), B=(wB, lB), Uu=(wUu, lUu), Ul=(wUl, lUl), Pu=(wPu, lPu), Pl=(wPl, lPl))
 
