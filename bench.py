@@ -16,17 +16,19 @@ call per step).
 Multi-GPU (one process per GPU): the metric line keeps BASELINE's C3 config per GPU — the global
 batch has O*N_gpus obstacles, rank r draws only its own C3-sized block (units [r*O*T,
 (r+1)*O*T)) with the device sampler and a step is its launch; units are independent
-(core/halfspaces.py:225-246), so there is no collective in the step (weak scaling, identical
-per-GPU work at every N).  The north-star form is the `strong_scaling` key, at every N: ONE
-global C5 batch (256 x 50 x 10 000) sharded over the ranks, a step = the shard's launch + an RCCL
-all_gather_into_tensor of the 64-B records to every rank (the exchange the QP hand-off needs,
-core/mpc_filter.py:116-151), and the full loop with the QP.  (A C3 step with the all-gather in
-it measures the all-gather: ~4 us of kernel against tens of us of collective latency.)
+(core/halfspaces.py:225-246), so there is no collective in the step: WEAK scaling, identical
+per-GPU work at every N, labelled so in `scaling` / `metric_form`.  The north-star form is the
+`strong_scaling` key, at every N, one leg per BASELINE config with a sharded batch: c4 (64 x 30 x
+5 000, 154 MB) and c5 (256 x 50 x 10 000, 2.05 GB) — ONE global batch sharded over the ranks, a
+step = the shard's launch + an RCCL all_gather_into_tensor of the 64-B records to every rank (the
+exchange the QP hand-off needs, core/mpc_filter.py:116-151).  Each leg also reports its phases
+alone, max over ranks (`phases_rank_max`: kernel_ms, allgather_ms), so a scaling curve can be
+read; c5 adds the full loop with the QP.
 
 Prints ONE JSON line on rank 0: value = units of all ranks / max rank time, plus
   roofline        the kernel on this workload: algorithmic bytes per launch / average launch time
                   (N=1: HIP events over the timed region / K, launch gaps included)
-  strong_scaling  C5 global batch sharded over N ranks (+ all-gather), value and full MPC loop
+  strong_scaling  {c4, c5}: global batch sharded over N ranks (+ all-gather), phase splits
   roofline_large  (N=1) the kernel on the resident 2 GB C5 batch, graph-replayed, event-timed
   cpu_baseline    oracle/drcvar_oracle.c (1 thread) on whole batches of the same workload
   max_abs_err     max |offset - oracle| over the benchmarked batch (the metric's second half)
@@ -130,24 +132,33 @@ def cpu_baseline(samples, ego, params, budget_s):
 
 
 class Stepper:
-    """Issues exactly the requested number of steps of a `ShardedBatch` (kernel, plus the RCCL
-    all-gather when world > 1): eager ctypes launches, or hipGraph replays — a graph of
-    G = min(graph_batch, steps) steps replayed steps // G times plus a graph of the remainder, so
-    the steps issued are the steps asked for."""
+    """Issues exactly the requested number of steps of a `ShardedBatch` — the kernel (`compute`)
+    and/or the RCCL all-gather (`exchange`, world > 1) — as eager ctypes launches, or as hipGraph
+    replays: a graph of G = min(graph_batch, steps) steps replayed steps // G times plus a graph
+    of the remainder (and one of the warm-up count), so the steps issued are the steps asked for.
+    If capturing fails (e.g. a collective the backend cannot capture) the stepper falls back to
+    eager launches in the same process and says so in describe()."""
 
-    def __init__(self, sb, mode, graph_batch, steps, dev, exchange=True):
-        self.sb, self.mode, self.dev, self.exchange = sb, mode, dev, exchange
+    def __init__(self, sb, mode, graph_batch, steps, dev, exchange=True, compute=True, warmup=0):
+        self.sb, self.mode, self.dev = sb, mode, dev
+        self.exchange = exchange and sb.full is not None
+        self.compute = compute
         self.G = max(1, min(graph_batch, steps)) if mode == "graph" else 1
-        self.rem = steps % self.G if mode == "graph" else 0
-        self.graphs, self._keep = {}, []
+        self.graphs, self._keep, self.fallback = {}, [], None
         if mode == "graph":
             self._one()                       # warm the code objects (and the communicator)
             torch.cuda.synchronize(dev)
-            for n in {self.G, self.rem} - {0}:
-                self.graphs[n] = self._capture(n)
+            try:
+                for n in sorted({self.G, steps % self.G, warmup % self.G} - {0}):
+                    self.graphs[n] = self._capture(n)
+            except Exception as exc:          # noqa: BLE001 - reported, then eager launches
+                self.mode, self.G, self.graphs = "eager", 1, {}
+                self.fallback = f"hipGraph capture failed ({type(exc).__name__}: {exc}); eager launches"
+                torch.cuda.synchronize(dev)
 
     def _one(self, launch=None):
-        self.sb.compute(launch)
+        if self.compute:
+            self.sb.compute(launch)
         if self.exchange:
             self.sb.exchange()
 
@@ -169,7 +180,7 @@ class Stepper:
             r = steps % self.G
             if r and r in self.graphs:
                 self.graphs[r].replay()
-            else:                             # (warmup counts other than the timed one)
+            else:
                 for _ in range(r):
                     self._one()
             return steps
@@ -178,10 +189,16 @@ class Stepper:
         return steps
 
     def describe(self):
-        what = "launch" + (" + RCCL all_gather_into_tensor" if self.exchange and self.sb.full is not None else "")
+        backend = dist.get_backend() if dist.is_initialized() else None
+        coll = f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend})"
+        parts = (["launch"] if self.compute else []) + ([coll] if self.exchange else [])
+        what = " + ".join(parts)
+        if self.fallback:
+            return f"{self.fallback}; step = {what}"
         if self.mode == "graph":
-            return (f"hipGraph replays of {self.G} steps (+ one of {self.rem})" if self.rem
-                    else f"hipGraph replays of {self.G} steps") + f"; step = {what}"
+            extra = sorted(set(self.graphs) - {self.G})
+            return (f"hipGraph replays of {self.G} steps" + (f" (+ graphs of {extra})" if extra else "")
+                    + f"; step = {what}")
         return f"eager; step = {what}"
 
 
@@ -211,20 +228,6 @@ def timed(world, fn, dev, stream):
     return elapsed, ev_s, res
 
 
-def kernel_only_time(sb, dev, stream, launches=400, graph_batch=50):
-    """Average duration of this rank's halfspace launch alone: HIP events around graph replays of
-    back-to-back launches (the form the rocprof kernel trace averages)."""
-    st = Stepper(sb, "graph", graph_batch, launches, dev, exchange=False)
-    st.run(launches)                          # warm
-    torch.cuda.synchronize(dev)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(stream)
-    st.run(launches)
-    b.record(stream)
-    torch.cuda.synchronize(dev)
-    return a.elapsed_time(b) * 1e-3 / launches
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,8 +236,8 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"])
     ap.add_argument("--graph-batch", type=int, default=50)
-    ap.add_argument("--strong-workload", default="c5", choices=sorted(WORKLOADS),
-                    help="global batch of the strong-scaling line (sharded over the ranks)")
+    ap.add_argument("--strong-workloads", default="c4,c5",
+                    help="global batches of the strong-scaling legs (sharded over the ranks), comma-separated")
     ap.add_argument("--strong-steps", type=int, default=20)
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -274,14 +277,15 @@ def main():
     ego = synthetic.straight_line_ego(T, dev)
     sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=42, gather_device=gdev)
     assert sb.count == O * T
-    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev, exchange=False)
-    stepper.run(args.warmup)                   # untimed warmup (W steps)
+    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev, exchange=False, warmup=args.warmup)
+    stepper.run(args.warmup)                   # untimed warmup (W steps, the same launch path)
     elapsed, ev_s, K = timed(world, lambda: stepper.run(args.steps), dev, stream)
     kernel_s, ktiming = ev_s / K, "HIP events over the timed region / K (launch gaps included)"
 
     strong = None
     if not args.no_large and not args.no_strong:
-        strong = strong_scaling(args, world, rank, dev, stream, params, gdev, mode)
+        strong = {w: strong_scaling(args, world, rank, dev, stream, params, gdev, mode, w)
+                  for w in args.strong_workloads.split(",") if w}
 
     result = None
     if rank == 0:
@@ -296,6 +300,10 @@ def main():
             "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
+            "metric_form": ("weak scaling: every rank evaluates its own C3-sized block of a global "
+                            f"{O * world}-obstacle batch, no collective in the step (units are "
+                            "independent); the north-star sharded form with the RCCL all-gather is "
+                            "strong_scaling"),
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (device-generated obstacle samples, SURVEY.md §8d distributions)",
@@ -311,18 +319,19 @@ def main():
             "strong_scaling": strong,
         }
     large = mpc = sampling = None
-    if rank == 0 and world == 1 and not args.no_large and strong is not None:
-        big = strong.pop("_batch")
-        large = strong.pop("_roofline")
+    c5leg = (strong or {}).get("c5")
+    if rank == 0 and world == 1 and not args.no_large and c5leg is not None:
+        big = c5leg.pop("_batch")
+        large = c5leg.pop("_roofline")
         sampling = sampler_roofline(big, stream)
         if not args.no_mpc:
             mpc = mpc_handoff(dev, big.samples.view(big.O, big.T, big.N, 2), big.ego_units[:big.T],
                               params, with_cpu=not args.no_cpu_baseline)
         del big
         torch.cuda.empty_cache()
-    elif strong is not None:
-        strong.pop("_batch", None)
-        strong.pop("_roofline", None)
+    for leg in (strong or {}).values():
+        leg.pop("_batch", None)
+        leg.pop("_roofline", None)
     if rank == 0:
         result["roofline_large"] = large
         result["mpc_handoff"] = mpc
@@ -346,34 +355,53 @@ def main():
     return result
 
 
-def strong_scaling(args, world, rank, dev, stream, params, gdev, mode):
-    """The north-star multi-GPU form (BASELINE configs 4/5): ONE global batch (default C5,
-    256 x 50 x 10 000, 2.05 GB) sharded over the ranks — each rank draws only its contiguous unit
-    block on its device, the kernel writes into its slice of the all-gather input and the records
-    are all-gathered over RCCL inside the timed region.  Identical global work at every N (strong
-    scaling); at N = 1 the exchange is the identity and is skipped.  Also times the full MPC loop
-    (shard kernel -> all-gather -> the DR-CVaR QP over all O*T halfspaces, replicated per rank)."""
-    O, T, N, desc = WORKLOADS[args.strong_workload]
-    nominal = synthetic.nominal_paths(O, T, dev, seed=7)
+def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload):
+    """The north-star multi-GPU form (BASELINE configs 4 and 5): ONE global batch sharded over
+    the ranks — each rank draws only its contiguous unit block on its device, the kernel writes
+    into its slice of the all-gather input and the records are all-gathered over RCCL inside the
+    timed region.  Identical global work at every N (strong scaling); at N = 1 the exchange is
+    the identity and is skipped.  Besides the whole step, each phase is timed alone and reported
+    as its maximum over the ranks: `kernel_ms` (the shard's launch) and `allgather_ms` (the
+    collective alone, the same records).  For C5 also the full MPC loop (shard kernel ->
+    all-gather -> the DR-CVaR QP over all O*T halfspaces, replicated per rank)."""
+    O, T, N, desc = WORKLOADS[workload]
+    seed = 7 if workload == "c5" else 11
+    nominal = synthetic.nominal_paths(O, T, dev, seed=seed)
     ego = synthetic.straight_line_ego(T, dev)
-    sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=7, gather_device=gdev)
+    sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed, gather_device=gdev)
     K = args.strong_steps
     st = Stepper(sb, mode, 10, K, dev)
     st.run(min(K, 10))
     elapsed, _, _ = timed(world, lambda: st.run(K), dev, stream)
-    kernel_s = kernel_only_time(sb, dev, stream, launches=20, graph_batch=10)
-    out = {"workload": f"{args.strong_workload}: {desc}, global batch sharded over {world} rank(s)",
+    launch = st.describe()
+    del st
+    # phases alone, rank-max (HIP events on the launching stream, K steps each)
+    kst = Stepper(sb, mode, 10, K, dev, exchange=False)
+    kst.run(min(K, 10))
+    _, kernel_s, _ = timed(world, lambda: kst.run(K), dev, stream)
+    del kst
+    gather_ms = None
+    if world > 1:
+        gst = Stepper(sb, mode, 10, K, dev, compute=False)
+        gst.run(min(K, 10))
+        _, gather_s, _ = timed(world, lambda: gst.run(K), dev, stream)
+        gather_ms = gather_s / K * 1e3
+        del gst
+    kernel_s /= K
+    out = {"workload": f"{workload}: {desc}, global batch sharded over {world} rank(s)",
            "value": sb.U * K / elapsed, "unit": "halfspace-constraints/s", "n_gpus": world,
            "steps": K, "ms_per_step": elapsed / K * 1e3, "scaling": "strong",
            "units_global": sb.U, "units_per_rank": sb.per,
+           "bytes_per_rank": sb.algorithmic_bytes,
+           "record_bytes_gathered": sb.per * world * 64 if world > 1 else 0,
            "parallelism": f"dp{world}" + (f"+allgather ({'RCCL' if gdev is None else 'gloo'})"
                                            if world > 1 else ""),
-           "launch": st.describe(),
-           "rank0_kernel_ms": kernel_s * 1e3,
-           "rank0_kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK}
-    del st
+           "launch": launch,
+           "phases_rank_max": {"kernel_ms": kernel_s * 1e3, "allgather_ms": gather_ms,
+                               "timing": f"HIP events over {K} steps of the phase alone, max over ranks"},
+           "kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK}
     # full loop: + the QP hand-off on every rank (core/mpc_filter.py:116-151 takes all halfspaces)
-    if not args.no_mpc:
+    if workload == "c5" and not args.no_mpc:
         import numpy as np
         from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
         dt = 0.2
@@ -407,12 +435,12 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode):
                             "qp": f"dr_cvar safety filter, H={T}, {sb.U} halfspace rows, one problem, "
                                   f"replicated on every rank",
                             "qp_status": mf.STATUS_NAMES.get(int(info[0])), "qp_iterations": int(info[1])}
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and workload == "c5":
         out["_batch"] = sb
         large = roofline(sb.algorithmic_bytes, kernel_s, load_traffic("c5"))
         large["workload"] = f"{O} obstacles x {T} steps x {N} samples (2.05 GB resident)"
         large["halfspaces_per_s"] = sb.U / kernel_s
-        large["timing"] = "HIP events over 20 graph-replayed launches (2 replays of 10)"
+        large["timing"] = f"HIP events over {K} graph-replayed launches (replays of 10)"
         out["_roofline"] = large
     return out
 
@@ -508,16 +536,9 @@ def mpc_handoff(dev, samples, ego, params, with_cpu):
     qp_ms = timed(qp, 5)
     info = res["info"][0].cpu().numpy()
     groups = model.launch_groups(1, O)
-    # the same QP on one workgroup (DRCVAR_MPC_CLUSTER=1), for comparison with the clustered launch
-    prev = os.environ.get("DRCVAR_MPC_CLUSTER")
-    os.environ["DRCVAR_MPC_CLUSTER"] = "1"
-    try:
-        qp1_ms = timed(qp, 3)
-    finally:
-        if prev is None:
-            del os.environ["DRCVAR_MPC_CLUSTER"]
-        else:
-            os.environ["DRCVAR_MPC_CLUSTER"] = prev
+    # the same QP on one workgroup (options.cluster_size = 1), for comparison with the clustered launch
+    one_wg = mf.make_options(cluster_size=1)
+    qp1_ms = timed(lambda: mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=one_wg), 3)
     qp()  # leaves the clustered answer in res
     c5 = {"workload": f"{O} obstacles x {T} steps x {samples.shape[2]} samples -> dr_cvar QP "
                       f"(H={H}, {O * T} halfspace rows), 1 problem",

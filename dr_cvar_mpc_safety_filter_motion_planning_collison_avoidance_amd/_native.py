@@ -25,11 +25,13 @@ HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("drcvar_halfspace.h", "drcvar_
                                                   "drcvar_sampling.h")]
 OFFLOAD_ARCH = os.environ.get("DRCVAR_OFFLOAD_ARCH", "gfx950")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OUT_WIDTH = 8
 MAX_SAMPLES = 16384               # largest unit held on chip (register plans)
 MAX_SAMPLES_STREAM = 2 ** 31 - 1  # larger units run the streaming kernel
 COL_MEAN_H0, COL_MEAN_H1, COL_G_MEAN, COL_H0, COL_H1, COL_G_CVAR, COL_G_DR_STAR, COL_G_DR_TILDE = range(8)
+# per-unit status word (DRCVAR_UNIT_*), a bit set
+UNIT_OK, UNIT_NONFINITE, UNIT_UNBOUNDED, UNIT_DR_UNBOUNDED = 0, 1, 2, 4
 
 # return codes (include/drcvar_halfspace.h)
 OK, ERR_INVALID_ARGUMENT, ERR_UNSUPPORTED, ERR_LAUNCH = 0, 1, 2, 3
@@ -40,7 +42,8 @@ MPC_INFO_WIDTH = 10
 (MPC_INFO_STATUS, MPC_INFO_ITERATIONS, MPC_INFO_OBJECTIVE, MPC_INFO_MU, MPC_INFO_PRIMAL_RES,
  MPC_INFO_DUAL_RES, MPC_INFO_MAX_SLACK, MPC_INFO_USED_FALLBACK, MPC_INFO_POLISHED,
  MPC_INFO_POLISH_ATTEMPTS) = range(10)
-MPC_STATUS_OPTIMAL, MPC_STATUS_MAX_ITER, MPC_STATUS_NUMERICAL, MPC_STATUS_OPTIMAL_INACCURATE = 0, 1, 2, 3
+(MPC_STATUS_OPTIMAL, MPC_STATUS_MAX_ITER, MPC_STATUS_NUMERICAL, MPC_STATUS_OPTIMAL_INACCURATE,
+ MPC_STATUS_CLUSTER_TIMEOUT, MPC_STATUS_CLUSTER_DIVERGED) = range(6)
 
 
 class MpcModel(ctypes.Structure):
@@ -54,18 +57,31 @@ class MpcModel(ctypes.Structure):
                 ("blob_doubles", ctypes.c_int64)]
 
 
+class MpcOptions(ctypes.Structure):
+    """``drcvar_mpc_options`` (include/drcvar_mpc.h): per-call options, all 0 = the defaults."""
+
+    _fields_ = [("cluster_size", ctypes.c_int32), ("spin_limit_us", ctypes.c_int32),
+                ("debug_force_resume", ctypes.c_int32), ("debug_perturb_group", ctypes.c_int32),
+                ("debug_perturb_iteration", ctypes.c_int32), ("debug_stall_group", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 2)]
+
+
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "drcvar_abi_version",
     "drcvar_strerror",
     "drcvar_safe_halfspaces_f64",
     "drcvar_safe_halfspaces_f64_ex",
+    "drcvar_safe_halfspaces_f64_v2",
     "drcvar_offsets_given_h_f64",
+    "drcvar_offsets_given_h_f64_v2",
     "drcvar_launch_plan",
     "drcvar_mpc_model_init",
     "drcvar_mpc_workspace_doubles",
     "drcvar_mpc_launch_groups",
+    "drcvar_mpc_launch_groups_ex",
     "drcvar_mpc_filter_f64",
+    "drcvar_mpc_filter_f64_ex",
     "drcvar_sample_trajectories_f64",
     "drcvar_sample_units_f64",
 )
@@ -87,30 +103,58 @@ _lock = threading.Lock()
 _lib = None
 
 
+def _compile_units():
+    """(source, extra defines) per object: the MPC source is compiled as five parts (host code,
+    then the kernels of the 1..4-input models: csrc/drcvar_mpc.hip, DRCVAR_MPC_PART) so that its
+    template instantiations build concurrently."""
+    units = []
+    for src in SOURCES:
+        if src.endswith("drcvar_mpc.hip"):
+            units += [(src, (f"-DDRCVAR_MPC_PART={k}",)) for k in range(5)]
+        else:
+            units.append((src, ()))
+    return units
+
+
 def build(verbose: bool = False, extra_flags=()) -> str:
-    """Compile the engine for gfx950 with hipcc into ``_lib/`` (works without a GPU)."""
+    """Compile the engine for gfx950 with hipcc into ``_lib/`` (works without a GPU).
+
+    One hipcc per translation unit, concurrently, then one link.  Objects are cached under
+    ``_lib/obj`` by a hash of the unit's source, the headers and the flags, so a rebuild after an
+    edit recompiles only the units it touched."""
+    import hashlib
     os.makedirs(LIB_DIR, exist_ok=True)
-    # one hipcc per source, concurrently (the halfspace kernel's template plans dominate), then
-    # one link: the library is the same as a single-command build
-    objs = [os.path.join(LIB_DIR, os.path.basename(src) + ".o") for src in SOURCES]
-    procs = []
-    for src, obj in zip(SOURCES, objs):
-        cmd = ["hipcc", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
-               "-I", INCLUDE_DIR, *extra_flags, src, "-o", obj]
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    headers = b"".join(open(h, "rb").read() for h in HEADERS)
+    objs, procs = [], []
+    for src, defs in _compile_units():
+        flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-I", INCLUDE_DIR,
+                 *defs, *extra_flags]
+        key = hashlib.sha256(open(src, "rb").read() + headers + " ".join(flags).encode()).hexdigest()[:16]
+        obj = os.path.join(obj_dir, f"{os.path.basename(src)}{''.join(defs).replace('-D', '.')}.{key}.o")
+        objs.append(obj)
+        if os.path.exists(obj):
+            continue
+        cmd = ["hipcc", *flags, src, "-o", obj + ".tmp"]
         if verbose:
             print(" ".join(cmd))
-        procs.append((cmd, subprocess.Popen(cmd)))
-    failed = [cmd for cmd, p in procs if p.wait() != 0]
+        procs.append((cmd, obj, subprocess.Popen(cmd)))
+    failed = [cmd for cmd, _, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
+    for _, obj, _ in procs:
+        os.replace(obj + ".tmp", obj)
     link = ["hipcc", f"--offload-arch={OFFLOAD_ARCH}", "-shared", "-fPIC", *objs,
             "-o", LIB_PATH + ".tmp"]
     if verbose:
         print(" ".join(link))
     subprocess.run(link, check=True)
-    for obj in objs:
-        os.remove(obj)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    keep = set(objs)  # drop stale cached objects
+    for f in os.listdir(obj_dir):
+        if os.path.join(obj_dir, f) not in keep:
+            os.remove(os.path.join(obj_dir, f))
     return LIB_PATH
 
 
@@ -130,6 +174,13 @@ def _bind(lib):
     lib.drcvar_offsets_given_h_f64.argtypes = [
         ptr, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr]
     lib.drcvar_offsets_given_h_f64.restype = ctypes.c_int
+    lib.drcvar_safe_halfspaces_f64_v2.argtypes = [
+        ptr, i64, i64, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr, ptr,
+        ctypes.c_int32, ctypes.c_int32]
+    lib.drcvar_safe_halfspaces_f64_v2.restype = ctypes.c_int
+    lib.drcvar_offsets_given_h_f64_v2.argtypes = [
+        ptr, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, ptr, ptr, ptr]
+    lib.drcvar_offsets_given_h_f64_v2.restype = ctypes.c_int
     lib.drcvar_launch_plan.argtypes = [i64, i32p, i32p, i32p]
     lib.drcvar_launch_plan.restype = ctypes.c_int
     i32, modelp = ctypes.c_int32, ctypes.POINTER(MpcModel)
@@ -144,6 +195,11 @@ def _bind(lib):
         modelp, ptr, i64, ptr, ptr, i64, i64, i64, i64, i64, i64, i64, i64, ptr, i64, ptr, i64,
         i64, ptr, i64, i64, i32, dbl, i32, ptr, ptr, ptr, ptr, i64, ptr]
     lib.drcvar_mpc_filter_f64.restype = ctypes.c_int
+    optp = ctypes.POINTER(MpcOptions)
+    lib.drcvar_mpc_launch_groups_ex.argtypes = [modelp, i64, i64, optp]
+    lib.drcvar_mpc_launch_groups_ex.restype = ctypes.c_int32
+    lib.drcvar_mpc_filter_f64_ex.argtypes = lib.drcvar_mpc_filter_f64.argtypes[:-1] + [optp, ptr]
+    lib.drcvar_mpc_filter_f64_ex.restype = ctypes.c_int
     u64 = ctypes.c_uint64
     lib.drcvar_sample_trajectories_f64.argtypes = [
         ptr, i64, i64, i64, i64, i64, dbl, dbl, dbl, u64, u64, i32, ptr, i64, i64, i64, ptr]

@@ -151,34 +151,32 @@ class HalfspaceBatch:
 
 def launch_with_singletons(launch, keys, shape, robot_radius, obstacle_radius):
     """Records of a grid of units whose CVaR / DR-CVaR parameters come from the reference's
-    N-keyed optimiser singletons (``risk_metrics.singleton_params``).
+    N-keyed optimiser singletons (``risk_metrics.plan_singletons``).
 
     ``launch(params) -> [*shape, 8]`` evaluates the whole grid with one parameter set; ``keys``
     lists ``((a_c, d_c), (a_d, d_d, e_d))`` per unit in row-major order of ``shape``.  Every
     column but ``g_cvar`` comes from the unit's DR-CVaR parameters (the directions and the mean
     halfspace do not depend on them), ``g_cvar`` from its CVaR parameters.  The usual case — one
     parameter set for the whole grid, CVaR equal to DR — is ONE launch; each further distinct
-    set costs one more launch of the grid.
+    set costs one more launch of the grid, and the rows are picked by one gather per column group
+    (each unit mapped once to the index of its parameter set).
     """
-    def pset(a, d, e):
-        return RiskParams(robot_radius, obstacle_radius, a, d, e)
-    dr_of = [pset(*dk) for _, dk in keys]
-    cv_of = [dr if ck == dk[:2] else pset(ck[0], ck[1], dk[2]) for (ck, dk), dr in zip(keys, dr_of)]
-    needed = list(dict.fromkeys(dr_of + cv_of))
-    recs = {p: launch(p) for p in needed}
-    first = recs[needed[0]]
+    index: dict = {}
+    dr_idx = np.empty(len(keys), dtype=np.int64)
+    cv_idx = np.empty(len(keys), dtype=np.int64)
+    for u, (ck, dk) in enumerate(keys):
+        dr_idx[u] = index.setdefault(dk, len(index))
+        cv_idx[u] = index.setdefault((ck[0], ck[1], dk[2]), len(index))
+    needed = [RiskParams(robot_radius, obstacle_radius, *k) for k in index]
+    recs = [launch(p) for p in needed]
     if len(needed) == 1:
-        return first
-    out = torch.empty_like(first)
-    flat = out.view(-1, engine.OUT_WIDTH)
-    for p, r in recs.items():                     # whole rows from the DR-CVaR parameters ...
-        m_dr = torch.as_tensor([q == p for q in dr_of], device=out.device)
-        flat[m_dr] = r.reshape(-1, engine.OUT_WIDTH)[m_dr]
-    col = flat[:, _native.COL_G_CVAR]
-    for p, r in recs.items():                     # ... then g_cvar from the CVaR parameters
-        m_cv = torch.as_tensor([q == p for q in cv_of], device=out.device)
-        col[m_cv] = r.reshape(-1, engine.OUT_WIDTH)[m_cv, _native.COL_G_CVAR]
-    return out
+        return recs[0]
+    flat = torch.stack([r.reshape(-1, engine.OUT_WIDTH) for r in recs])   # [P, U, 8]
+    dev = flat.device
+    units = torch.arange(flat.shape[1], device=dev)
+    out = flat[torch.as_tensor(dr_idx, device=dev), units]                 # whole rows: DR params
+    out[:, _native.COL_G_CVAR] = flat[torch.as_tensor(cv_idx, device=dev), units, _native.COL_G_CVAR]
+    return out.view(recs[0].shape)
 
 
 def compute_safe_halfspaces_batched(samples, ego, robot_radius, obstacle_radius, alpha, delta,
@@ -222,7 +220,7 @@ def compute_safe_halfspaces(obstacle_samples, ego_ref_pos, robot_radius, obstacl
     t0 = time.time()
     dev = risk_metrics.device()
     counts = [int(np.shape(s)[0]) for s in obstacle_samples]
-    keys = risk_metrics.singleton_params(counts, alpha, delta, epsilon)
+    keys, final = risk_metrics.plan_singletons(counts, alpha, delta, epsilon)
     groups: dict[int, list[int]] = {}
     for i, n in enumerate(counts):
         groups.setdefault(n, []).append(i)
@@ -238,6 +236,7 @@ def compute_safe_halfspaces(obstacle_samples, ego_ref_pos, robot_radius, obstacl
             for idx, s in staged]
     host_recs = [(idx, r.cpu().numpy()) for idx, r in recs]
     t2 = time.time()
+    risk_metrics.commit_singletons(final)  # only once every launch has succeeded
     per = {"setup_time": (t1 - t0) / n_obstacles, "solve_time": (t2 - t1) / n_obstacles}
     per["solve_call_time"] = per["setup_time"] + per["solve_time"]
     for idx, rec in host_recs:

@@ -30,7 +30,9 @@ from . import risk_metrics
 
 STATUS_NAMES = {_native.MPC_STATUS_OPTIMAL: "optimal", _native.MPC_STATUS_MAX_ITER: "max_iter",
                 _native.MPC_STATUS_NUMERICAL: "numerical_error",
-                _native.MPC_STATUS_OPTIMAL_INACCURATE: "optimal_inaccurate"}
+                _native.MPC_STATUS_OPTIMAL_INACCURATE: "optimal_inaccurate",
+                _native.MPC_STATUS_CLUSTER_TIMEOUT: "cluster_timeout",
+                _native.MPC_STATUS_CLUSTER_DIVERGED: "cluster_diverged"}
 SOLVED = ("optimal", "optimal_inaccurate")   # core/mpc_filter.py:154
 # record columns of each metric's (h, g): core/halfspaces.py get_constraint_params
 METRIC_COLUMNS = {"mean": (_native.COL_MEAN_H0, _native.COL_G_MEAN),
@@ -58,6 +60,24 @@ def _host(m):
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def make_options(cluster_size=0, spin_limit_us=0, debug_force_resume=False, debug_perturb_group=None,
+                 debug_perturb_iteration=0, debug_stall_group=None) -> _native.MpcOptions:
+    """``drcvar_mpc_options`` (include/drcvar_mpc.h).  ``cluster_size`` 0 = automatic, 1 = one
+    workgroup per problem; the ``debug_*`` hooks exist for the tests (groups are 0-based here)."""
+    o = _native.MpcOptions()
+    o.cluster_size = int(cluster_size)
+    o.spin_limit_us = int(spin_limit_us)
+    o.debug_force_resume = int(bool(debug_force_resume))
+    o.debug_perturb_group = 0 if debug_perturb_group is None else int(debug_perturb_group) + 1
+    o.debug_perturb_iteration = int(debug_perturb_iteration)
+    o.debug_stall_group = 0 if debug_stall_group is None else int(debug_stall_group) + 1
+    return o
+
+
+def _opt_ref(options):
+    return ctypes.byref(options) if options is not None else None
 
 
 class MPCModel:
@@ -88,10 +108,10 @@ class MPCModel:
         self.A, self.B = A, B
         self.nx, self.nu, self.horizon = nx, nu, int(horizon)
 
-    def launch_groups(self, n_problems, n_obstacles):
-        """Workgroups per problem a launch of this batch shape uses (drcvar_mpc_launch_groups)."""
-        return int(_native.lib().drcvar_mpc_launch_groups(ctypes.byref(self.model), n_problems,
-                                                          n_obstacles))
+    def launch_groups(self, n_problems, n_obstacles, options=None):
+        """Workgroups per problem a launch of this batch shape uses (drcvar_mpc_launch_groups_ex)."""
+        return int(_native.lib().drcvar_mpc_launch_groups_ex(ctypes.byref(self.model), n_problems,
+                                                             n_obstacles, _opt_ref(options)))
 
     def workspace_doubles(self, n_problems, n_obstacles):
         return int(_native.lib().drcvar_mpc_workspace_doubles(ctypes.byref(self.model), n_problems,
@@ -110,13 +130,13 @@ def _check_dev(t, name, shape, device):
 def filter_batch(model: MPCModel, hs_h: torch.Tensor, hs_g: torch.Tensor, x0: torch.Tensor,
                  x_ref: torch.Tensor, u_fallback: torch.Tensor, max_iter: int = DEFAULT_MAX_ITER,
                  tol: float = DEFAULT_TOL, polish: bool = True,
-                 workspace: torch.Tensor | None = None, stream=None):
-    """Solve B safety-filter QPs on the device (one ``drcvar_mpc_filter_f64`` launch).
+                 workspace: torch.Tensor | None = None, stream=None, options=None):
+    """Solve B safety-filter QPs on the device (one ``drcvar_mpc_filter_f64_ex`` launch).
 
     hs_h [B, O, K, 2] (any strides, last 1), hs_g [B, O, K]; x0 [B, nx]; x_ref [B, H+1, nx];
     u_fallback [B, H, nu].  Returns (x [B, H+1, nx], u [B, H, nu], info [B, 10]) device tensors
     (columns ``_native.MPC_INFO_*``); nothing is synchronised.  ``polish`` finishes each solve
-    with the active-set polish (exact optimum when it succeeds).
+    with the active-set polish (exact optimum when it succeeds).  ``options``: :func:`make_options`.
     """
     dev = model.device
     B = x0.shape[0]
@@ -140,14 +160,14 @@ def filter_batch(model: MPCModel, hs_h: torch.Tensor, hs_g: torch.Tensor, x0: to
         return x, u, info
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     vp = ctypes.c_void_p
-    _native.check(_native.lib().drcvar_mpc_filter_f64(
+    _native.check(_native.lib().drcvar_mpc_filter_f64_ex(
         ctypes.byref(model.model), vp(model.blob.data_ptr()), B,
         vp(hs_h.data_ptr()), vp(hs_g.data_ptr()), O, K,
         hs_h.stride(0), hs_h.stride(1), hs_h.stride(2), hs_g.stride(0), hs_g.stride(1), hs_g.stride(2),
         vp(x0.data_ptr()), x0.stride(0), vp(x_ref.data_ptr()), x_ref.stride(0), x_ref.stride(1),
         vp(u_fallback.data_ptr()), u_fallback.stride(0), u_fallback.stride(1),
         int(max_iter), float(tol), int(bool(polish)), vp(x.data_ptr()), vp(u.data_ptr()), vp(info.data_ptr()),
-        vp(workspace.data_ptr()), workspace.numel(), vp(int(s.cuda_stream))))
+        vp(workspace.data_ptr()), workspace.numel(), _opt_ref(options), vp(int(s.cuda_stream))))
     return x, u, info
 
 

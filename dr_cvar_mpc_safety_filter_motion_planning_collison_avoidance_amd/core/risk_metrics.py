@@ -15,8 +15,9 @@ contract, but there is no LP to build: the GPU kernel evaluates the LP optimum i
 * ``tmp/timing_info_{drcvar,cvar}.json`` side channel with ``setup_time`` / ``solve_time`` seconds
   (:16-33), which ``core/halfspaces.py`` and ``evaluation/timing_analysis.py`` read back;
 * solver-failure sentinels (:173-177, :261-265, :298-303, :334-338): ``g = 100.0`` and
-  ``g_tilde = 100.0 - R_c|h|`` when the samples are not finite or the LP is unbounded
-  (alpha > 1; epsilon < 0 for DR-CVaR).
+  ``g_tilde = 100.0 - R_c|h|`` when the samples are not finite (or their sums overflow) or the LP
+  is unbounded (alpha > 1; epsilon < 0 for DR-CVaR).  Failure is what the kernel reports in its
+  per-unit status word (``_native.UNIT_*``), never inferred from the sentinel's value.
 
 ``RiskMetric`` is the batched evaluator named by the build's north star (no such class exists in
 the reference): one object per metric, ``evaluate(samples [O,T,N,2], ego [T,2])`` on device tensors.
@@ -56,6 +57,20 @@ def device() -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+_CVAR_FAILED = _native.UNIT_NONFINITE | _native.UNIT_UNBOUNDED
+_DR_FAILED = _CVAR_FAILED | _native.UNIT_DR_UNBOUNDED
+
+
+def failure_status(bits: int, dr: bool) -> str | None:
+    """The LP status name the reference would print for a unit's status bits, or None if solved
+    (ECOS reports an unbounded LP as dual infeasible and non-finite data as an error)."""
+    if bits & _native.UNIT_NONFINITE:
+        return "solver_error"
+    if bits & _native.UNIT_UNBOUNDED or (dr and bits & _native.UNIT_DR_UNBOUNDED):
+        return "unbounded"
+    return None
+
+
 def _stage_unit(h, samples, dev):
     s = torch.as_tensor(np.ascontiguousarray(samples, dtype=np.float64)).to(dev)
     hh = torch.as_tensor(np.ascontiguousarray(np.asarray(h, dtype=np.float64).reshape(1, 2))).to(dev)
@@ -80,14 +95,17 @@ class _UnitOptimizer:
         s, hh = _stage_unit(h, samples, dev)
         setup_time = time.time() - setup_start
         solve_start = time.time()
-        out = engine.offsets_given_h(s, hh, RiskParams(rc, 0.0, self.alpha, self.delta, self.epsilon))
+        st = torch.empty(1, dtype=torch.int32, device=dev)
+        out = engine.offsets_given_h(s, hh, RiskParams(rc, 0.0, self.alpha, self.delta, self.epsilon),
+                                     status=st)
         rec = out[0].cpu().numpy()
+        bits = int(st[0])
         solve_time = time.time() - solve_start
         info = {"setup_time": setup_time, "solve_time": solve_time,
                 "solve_call_time": setup_time + solve_time}
         if WRITE_TIMING_FILES:
             save_timing_info(self.key, setup_time, solve_time)
-        return rec, info
+        return rec, bits, info
 
 
 class DRCVaROptimizer(_UnitOptimizer):
@@ -101,16 +119,12 @@ class DRCVaROptimizer(_UnitOptimizer):
 
     def solve(self, h, samples, combined_radius):
         # kernel with zero radius gives g*(r=0); the LP optimum is affine in r with slope 1 (:113-119)
-        rec, info = self._run(h, samples, 0.0)
-        g0 = float(rec[_native.COL_G_DR_STAR])
-        if g0 == 100.0 and not self._bounded(samples):
-            print(f"Warning: DR-CVaR optimization failed with status: unbounded_or_invalid")
+        rec, bits, info = self._run(h, samples, 0.0)
+        failed = failure_status(bits, dr=True)
+        if failed:                                                   # :173-177
+            print(f"Warning: DR-CVaR optimization failed with status: {failed}")
             return False, 100.0, info
-        return True, float(combined_radius) + g0, info
-
-    def _bounded(self, samples):
-        return (self.alpha <= 1.0 and self.epsilon >= 0.0
-                and bool(np.isfinite(np.asarray(samples, dtype=np.float64)).all()))
+        return True, float(combined_radius) + float(rec[_native.COL_G_DR_STAR]), info
 
 
 class CVaROptimizer(_UnitOptimizer):
@@ -123,13 +137,12 @@ class CVaROptimizer(_UnitOptimizer):
         super().__init__(alpha, 0.0, delta, max_samples)
 
     def solve(self, h, samples, combined_radius):
-        rec, info = self._run(h, samples, float(combined_radius))
-        g = float(rec[_native.COL_G_CVAR])
-        if g == 100.0 and not (self.alpha <= 1.0 and
-                               bool(np.isfinite(np.asarray(samples, dtype=np.float64)).all())):
-            print(f"Warning: CVaR optimization failed with status: unbounded_or_invalid")
+        rec, bits, info = self._run(h, samples, float(combined_radius))
+        failed = failure_status(bits, dr=False)
+        if failed:                                                   # :261-265
+            print(f"Warning: CVaR optimization failed with status: {failed}")
             return False, 100.0, info
-        return True, g, info
+        return True, float(rec[_native.COL_G_CVAR]), info
 
 
 def dr_cvar_halfspace(samples, h, alpha, delta, epsilon, robot_radius, obstacle_radius):
@@ -154,28 +167,43 @@ def cvar_halfspace(samples, h, alpha, delta, robot_radius, obstacle_radius):
     return g_value if solved else 100.0
 
 
-def singleton_params(sample_counts, alpha, delta, epsilon):
-    """The parameters the reference's optimiser singletons solve each call with.
+def plan_singletons(sample_counts, alpha, delta, epsilon):
+    """The parameters the reference's optimiser singletons solve each call with — without
+    touching them.
 
     The reference reaches its LPs only through ``cvar_halfspace`` / ``dr_cvar_halfspace``, whose
     module singletons are keyed on N alone (:289, :325): a call whose N matches the live singleton
     keeps the alpha/delta(/epsilon) the singleton was built with, any other N rebuilds it with the
     call's values — CVaR and DR-CVaR independently.  ``sample_counts`` lists N for every solve in
     the reference's call order (per ``compute_safe_halfspaces`` call: obstacles in order; per
-    ``compute_safe_halfspaces_for_trajectory``: steps outer, obstacles inner).  The singletons are
-    updated exactly as those calls would leave them.  Returns per call
-    ``((alpha_cvar, delta_cvar), (alpha_dr, delta_dr, epsilon_dr))``.
+    ``compute_safe_halfspaces_for_trajectory``: steps outer, obstacles inner).  Returns
+    ``(keys, final)``: per call ``((alpha_cvar, delta_cvar), (alpha_dr, delta_dr, epsilon_dr))``,
+    and the singletons as those calls leave them (hand to :func:`commit_singletons` once the
+    evaluation has succeeded).
     """
-    global drcvar_optimizer, cvar_optimizer
+    dr, cv = drcvar_optimizer, cvar_optimizer
     keys = []
     for n in sample_counts:
         n = int(n)
-        if drcvar_optimizer is None or drcvar_optimizer.n_samples != n:
-            drcvar_optimizer = DRCVaROptimizer(alpha, epsilon, delta, n)
-        if cvar_optimizer is None or cvar_optimizer.n_samples != n:
-            cvar_optimizer = CVaROptimizer(alpha, delta, n)
-        keys.append(((cvar_optimizer.alpha, cvar_optimizer.delta),
-                     (drcvar_optimizer.alpha, drcvar_optimizer.delta, drcvar_optimizer.epsilon)))
+        if dr is None or dr.n_samples != n:
+            dr = DRCVaROptimizer(alpha, epsilon, delta, n)
+        if cv is None or cv.n_samples != n:
+            cv = CVaROptimizer(alpha, delta, n)
+        keys.append(((cv.alpha, cv.delta), (dr.alpha, dr.delta, dr.epsilon)))
+    return keys, (dr, cv)
+
+
+def commit_singletons(final) -> None:
+    """Leave the singletons as :func:`plan_singletons` computed (after the launches succeeded)."""
+    global drcvar_optimizer, cvar_optimizer
+    drcvar_optimizer, cvar_optimizer = final
+
+
+def singleton_params(sample_counts, alpha, delta, epsilon):
+    """:func:`plan_singletons` + :func:`commit_singletons`: the per-call parameters, with the
+    singletons updated exactly as the reference's calls would leave them."""
+    keys, final = plan_singletons(sample_counts, alpha, delta, epsilon)
+    commit_singletons(final)
     return keys
 
 

@@ -690,6 +690,14 @@ __device__ __forceinline__ double norm_h(double h0, double h1) {
   return sqrt(n2);
 }
 
+// Per-unit status word (DRCVAR_UNIT_*): which of the reference's solver-failure branches the unit
+// took (core/risk_metrics.py:173-177,261-265: the LP status; :298-303,334-338: the sentinels) —
+// reported by the kernel itself, so no caller has to infer it from the sentinel's value.
+__device__ __forceinline__ int32_t failure_status(bool nonfinite, const Params& prm) {
+  return (nonfinite ? DRCVAR_UNIT_NONFINITE : 0) | (prm.unbounded ? DRCVAR_UNIT_UNBOUNDED : 0) |
+         (prm.epsilon < 0.0 ? DRCVAR_UNIT_DR_UNBOUNDED : 0);
+}
+
 // Offsets from the lower-tail statistics (wave 0, lane 0 writes).  L = tau + dsum / k.
 // r = R_c |h| (risk_metrics.py:293, :234), computed by the caller as soon as h is known.
 template <int NW>
@@ -731,7 +739,7 @@ __global__ void __launch_bounds__(BLOCK)
 safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
                       int64_t s_obs, int64_t s_step, int64_t s_samp,
                       const double* __restrict__ dir, int64_t dir_s_obs, int64_t dir_s_step,
-                      Params prm, double* __restrict__ out) {
+                      Params prm, double* __restrict__ out, int32_t* __restrict__ status) {
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << LOG_NB;
   __shared__ uint32_t hist[hist_words<NB>()];
@@ -846,6 +854,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       double m0, m1, g_mean;
       mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
       store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
+      if (status) status[u] = failure_status(bad, prm);
     }
     return;  // uniform across the workgroup
   }
@@ -986,6 +995,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 
   // ---- 5. offsets (wave 0) -------------------------------------------------------------------
   finish_offsets<NW>(rec, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
+  if (status && lane == 0) status[u] = failure_status(false, prm);
   DRCVAR_STAMP(7);
 }
 
@@ -1004,7 +1014,8 @@ __global__ void __launch_bounds__(kStreamBlock)
 safe_halfspace_stream_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
                              int64_t s_obs, int64_t s_step, int64_t s_samp,
                              const double* __restrict__ dir, int64_t dir_s_obs,
-                             int64_t dir_s_step, Params prm, double* __restrict__ out) {
+                             int64_t dir_s_step, Params prm, double* __restrict__ out,
+                             int32_t* __restrict__ status) {
   constexpr int BLOCK = kStreamBlock;
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << kStreamLogNB;
@@ -1052,6 +1063,7 @@ safe_halfspace_stream_kernel(const double* __restrict__ samples, int64_t n_steps
       double m0, m1, g_mean;
       mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
       store_record(rec, m0, m1, g_mean, h0, h1, kSentinel, kSentinel, kSentinel - r);
+      if (status) status[u] = failure_status(bad, prm);
     }
     return;
   }
@@ -1064,6 +1076,7 @@ safe_halfspace_stream_kernel(const double* __restrict__ samples, int64_t n_steps
     return;
   }
   finish_offsets<NW>(rec, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
+  if (status && lane == 0) status[u] = failure_status(false, prm);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1112,6 +1125,7 @@ struct Launch {
   int64_t dir_s_obs, dir_s_step;
   Params prm;
   double* out;
+  int32_t* status;  // [units] or null
   hipStream_t stream;
 };
 
@@ -1129,7 +1143,8 @@ void launch_form(const Launch& L) {
                        dim3(BLOCK), 0, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
                        static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
                        L.dir + o0 * L.dir_s_obs, L.dir_s_obs, L.dir_s_step, L.prm,
-                       L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH);
+                       L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH,
+                       L.status ? L.status + o0 * L.n_steps : nullptr);
   }
 }
 
@@ -1155,11 +1170,11 @@ void launch_stream(const Launch& L, bool vec) {
   if (vec) {
     hipLaunchKernelGGL((safe_halfspace_stream_kernel<true, GIVEN_H>), grid, block, 0, L.stream,
                        L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
-                       L.dir, L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+                       L.dir, L.dir_s_obs, L.dir_s_step, L.prm, L.out, L.status);
   } else {
     hipLaunchKernelGGL((safe_halfspace_stream_kernel<false, GIVEN_H>), grid, block, 0, L.stream,
                        L.samples, L.n_steps, static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
-                       L.dir, L.dir_s_obs, L.dir_s_step, L.prm, L.out);
+                       L.dir, L.dir_s_obs, L.dir_s_step, L.prm, L.out, L.status);
   }
 }
 
@@ -1258,7 +1273,8 @@ int safe_halfspaces(const double* samples, int64_t n_obstacles, int64_t n_steps,
                     int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
                     int64_t stride_sample, const double* ego_ref_pos, int64_t ego_stride_step,
                     double robot_radius, double obstacle_radius, double alpha, double delta,
-                    double epsilon, double* out, void* stream, int threads, int per) {
+                    double epsilon, double* out, int32_t* status, void* stream, int threads,
+                    int per) {
   if (n_obstacles < 0 || n_steps < 0 || n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (!params_ok(robot_radius, obstacle_radius, alpha, delta, epsilon))
     return DRCVAR_ERR_INVALID_ARGUMENT;
@@ -1268,7 +1284,7 @@ int safe_halfspaces(const double* samples, int64_t n_obstacles, int64_t n_steps,
   Launch L{samples, units, n_steps, n_samples, stride_obstacle, stride_step, stride_sample,
            ego_ref_pos, 0, ego_stride_step,
            make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
-           static_cast<hipStream_t>(stream)};
+           status, static_cast<hipStream_t>(stream)};
   return dispatch<false>(L, threads, per);
 }
 
@@ -1323,7 +1339,7 @@ int drcvar_safe_halfspaces_f64(const double* samples, int64_t n_obstacles, int64
                                double* out, void* stream) {
   return safe_halfspaces(samples, n_obstacles, n_steps, n_samples, stride_obstacle, stride_step,
                          stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
-                         obstacle_radius, alpha, delta, epsilon, out, stream, 0, 0);
+                         obstacle_radius, alpha, delta, epsilon, out, nullptr, stream, 0, 0);
 }
 
 int drcvar_safe_halfspaces_f64_ex(const double* samples, int64_t n_obstacles, int64_t n_steps,
@@ -1336,15 +1352,29 @@ int drcvar_safe_halfspaces_f64_ex(const double* samples, int64_t n_obstacles, in
   if ((threads_per_unit == 0) != (samples_per_thread == 0)) return DRCVAR_ERR_INVALID_ARGUMENT;
   return safe_halfspaces(samples, n_obstacles, n_steps, n_samples, stride_obstacle, stride_step,
                          stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
-                         obstacle_radius, alpha, delta, epsilon, out, stream, threads_per_unit,
-                         samples_per_thread);
+                         obstacle_radius, alpha, delta, epsilon, out, nullptr, stream,
+                         threads_per_unit, samples_per_thread);
 }
 
-int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n_samples,
-                               int64_t stride_unit, int64_t stride_sample, const double* h,
-                               int64_t h_stride_unit, double robot_radius, double obstacle_radius,
-                               double alpha, double delta, double epsilon, double* out,
-                               void* stream) {
+int drcvar_safe_halfspaces_f64_v2(const double* samples, int64_t n_obstacles, int64_t n_steps,
+                                  int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
+                                  int64_t stride_sample, const double* ego_ref_pos,
+                                  int64_t ego_stride_step, double robot_radius,
+                                  double obstacle_radius, double alpha, double delta,
+                                  double epsilon, double* out, int32_t* status, void* stream,
+                                  int32_t threads_per_unit, int32_t samples_per_thread) {
+  if ((threads_per_unit == 0) != (samples_per_thread == 0)) return DRCVAR_ERR_INVALID_ARGUMENT;
+  return safe_halfspaces(samples, n_obstacles, n_steps, n_samples, stride_obstacle, stride_step,
+                         stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
+                         obstacle_radius, alpha, delta, epsilon, out, status, stream,
+                         threads_per_unit, samples_per_thread);
+}
+
+int drcvar_offsets_given_h_f64_v2(const double* samples, int64_t n_units, int64_t n_samples,
+                                  int64_t stride_unit, int64_t stride_sample, const double* h,
+                                  int64_t h_stride_unit, double robot_radius,
+                                  double obstacle_radius, double alpha, double delta,
+                                  double epsilon, double* out, int32_t* status, void* stream) {
   if (n_units < 0 || n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (!params_ok(robot_radius, obstacle_radius, alpha, delta, epsilon))
     return DRCVAR_ERR_INVALID_ARGUMENT;
@@ -1354,8 +1384,18 @@ int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n
   Launch L{samples, n_units, n_units, n_samples, 0, stride_unit, stride_sample,
            h, 0, h_stride_unit,
            make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
-           static_cast<hipStream_t>(stream)};
+           status, static_cast<hipStream_t>(stream)};
   return dispatch<true>(L, 0, 0);
+}
+
+int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n_samples,
+                               int64_t stride_unit, int64_t stride_sample, const double* h,
+                               int64_t h_stride_unit, double robot_radius, double obstacle_radius,
+                               double alpha, double delta, double epsilon, double* out,
+                               void* stream) {
+  return drcvar_offsets_given_h_f64_v2(samples, n_units, n_samples, stride_unit, stride_sample, h,
+                                       h_stride_unit, robot_radius, obstacle_radius, alpha, delta,
+                                       epsilon, out, nullptr, stream);
 }
 
 }  // extern "C"

@@ -41,72 +41,28 @@
 
 #include "drcvar_mpc.h"
 
-namespace {
-
-// Threads per problem: 256 for batches (two workgroups per CU), 512 for launches of a few
-// problems (two waves per SIMD hide the row passes' fp64 latency; the chip has CUs to spare).
-// Device code below is written against kBlock / kWaves, which the kernel defines from its
-// BLK parameter; helpers take the wave count as a template argument.
-constexpr int kMaxWaves = 8;
-constexpr int kFewProblems = 128;  // at most this many problems per launch: 512-thread form
-constexpr int kShortHorizon = 32;  // horizon capacity of the 128-thread (many problems) form
-constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
-// h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s, then s and w_hs saved across a failed polish
-constexpr int kRowArrays = 10;
-// per workgroup: the best iterate u (n <= DRCVAR_MPC_MAX_DECISION, padded to 128), then the bound
-// states saved across a failed polish (bx [4 n], px [8 H]: <= 992)
-constexpr int kBestPad = 128 + 1024;
-constexpr int kRowStride = kRowArrays * kStepPad;  // one obstacle's block of the workspace
-constexpr double kSlackLin = 50.0;    // core/mpc_filter.py:143
-constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:144
-constexpr double kStepFrac = 0.995;
-constexpr double kHuge = 1e300;
-constexpr int kPerStepQ = 7;          // per-step partial sums carried by one reduction
-constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
-constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
-constexpr int kPolishAttempts = 6;    // active-set corrections
-constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
-constexpr double kPolishDualTol = 1e-7;
-constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
-constexpr int kResumeIters = 8;         // interior-point iterations after a failed polish
-constexpr double kResumeTol = 1e-3;     // ... towards tol * kResumeTol
-constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
-
-#ifdef DRCVAR_MPC_STAMPS
-// diagnostic build only: per-category shader-clock totals of problem 0..kStampProblems-1
-constexpr int kStampProblems = 64, kStampSlots = 20;
-__device__ unsigned long long g_mpc_stamps[kStampProblems * kStampSlots];
-__device__ unsigned long long g_cl_stamps[8];  // cluster exchange sub-phases, problem 0, group 0
-#define CL_STAMP(k)                                                     \
-  do {                                                                  \
-    if (threadIdx.x == 0 && blockIdx.x == 0) {                          \
-      const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
-      g_cl_stamps[(k)] += now_ - cl_t0;                                 \
-      cl_t0 = now_;                                                     \
-    }                                                                   \
-  } while (0)
-#define MPC_PHASE(k)                                                    \
-  do {                                                                  \
-    if (threadIdx.x == 0) {                                             \
-      const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
-      stamp_acc[(k)] += now_ - stamp_last;                              \
-      stamp_last = now_;                                                \
-    }                                                                   \
-  } while (0)
+// Build parts (compile time of the kernel templates): without DRCVAR_MPC_PART this file is the
+// whole library part; with -DDRCVAR_MPC_PART=0 only the host code (model condensing, queries,
+// argument checks), with -DDRCVAR_MPC_PART=k (1..4) only the kernels of the k-input models and
+// their launcher.  _native.build() compiles the five parts concurrently.
+#if !defined(DRCVAR_MPC_PART)
+#define DRCVAR_MPC_HOST_PART 1
+#define DRCVAR_MPC_DEVICE_PART(k) 1
 #else
-#define CL_STAMP(k) \
-  do {              \
-  } while (0)
-#define MPC_PHASE(k) \
-  do {               \
-  } while (0)
+#define DRCVAR_MPC_HOST_PART (DRCVAR_MPC_PART == 0)
+#define DRCVAR_MPC_DEVICE_PART(k) (DRCVAR_MPC_PART == (k))
 #endif
+#define DRCVAR_MPC_ANY_DEVICE_PART \
+  (DRCVAR_MPC_DEVICE_PART(1) || DRCVAR_MPC_DEVICE_PART(2) || DRCVAR_MPC_DEVICE_PART(3) || DRCVAR_MPC_DEVICE_PART(4))
+
+// types shared by the parts (the launch arguments cross from the host part to the kernel parts)
+namespace drcvar_mpc_detail {
 
 struct BlobLayout {
   int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, total;
 };
 
-BlobLayout blob_layout(int nx, int nu, int H) {
+inline BlobLayout blob_layout(int nx, int nu, int H) {
   const int64_t n = static_cast<int64_t>(nu) * H;
   BlobLayout L{};
   int64_t o = 0;
@@ -145,12 +101,112 @@ struct MpcArgs {
   double* ws;
   int64_t ws_off, ws_pp;  // per-problem region b at ws + ws_off + b * ws_pp
   int cl_size;            // workgroups per problem (clustered form)
-  int force_resume;       // test hook (DRCVAR_MPC_FORCE_RESUME=1): the first polish makes no attempt
+  uint64_t spin_ticks;    // bound of one cluster wait, in ticks of the 100 MHz s_memrealtime clock
+  // test hooks (drcvar_mpc_options.debug_*; 0 = off): the first polish makes no attempt; workgroup
+  // perturb_group - 1 scales its step length at iteration perturb_iter; workgroup stall_group - 1
+  // leaves before the final exchange
+  int force_resume, perturb_group, perturb_iter, stall_group;
   int max_iter;
   double tol;
   int polish;
 };
 
+// one launcher per input count, each defined in its own part
+int launch_nu1(const MpcArgs& args, int64_t n_problems, hipStream_t stream);
+int launch_nu2(const MpcArgs& args, int64_t n_problems, hipStream_t stream);
+int launch_nu3(const MpcArgs& args, int64_t n_problems, hipStream_t stream);
+int launch_nu4(const MpcArgs& args, int64_t n_problems, hipStream_t stream);
+int device_cus();
+
+}  // namespace drcvar_mpc_detail
+
+namespace {
+using namespace drcvar_mpc_detail;
+
+// Threads per problem: 256 for batches (two workgroups per CU), 512 for launches of a few
+// problems (two waves per SIMD hide the row passes' fp64 latency; the chip has CUs to spare).
+// Device code below is written against kBlock / kWaves, which the kernel defines from its
+// BLK parameter; helpers take the wave count as a template argument.
+constexpr int kMaxWaves = 8;
+constexpr int kFewProblems = 128;  // at most this many problems per launch: 512-thread form
+constexpr int kShortHorizon = 32;  // horizon capacity of the 128-thread (many problems) form
+constexpr int kStepPad = 64;  // workspace pitch: one lane per halfspace step
+// h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s, then s and w_hs saved across a failed polish
+constexpr int kRowArrays = 10;
+// per workgroup: the best iterate u (n <= DRCVAR_MPC_MAX_DECISION, padded to 128), then the bound
+// states saved across a failed polish (bx [4 n], px [8 H]: <= 992)
+constexpr int kBestPad = 128 + 1024;
+constexpr int kRowStride = kRowArrays * kStepPad;  // one obstacle's block of the workspace
+constexpr double kSlackLin = 50.0;    // core/mpc_filter.py:143
+constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:144
+constexpr double kStepFrac = 0.995;
+constexpr double kHuge = 1e300;
+constexpr int kPerStepQ = 7;          // per-step partial sums carried by one reduction
+constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
+constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
+constexpr int kPolishAttempts = 6;    // active-set corrections
+constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
+constexpr double kPolishDualTol = 1e-7;
+constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
+constexpr int kResumeIters = 8;         // interior-point iterations after a failed polish
+constexpr double kResumeTol = 1e-3;     // ... towards tol * kResumeTol
+constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
+
+// clustered form (see cluster_combine)
+constexpr int kClusterMaxProblems = 8;
+constexpr int kClusterMinObstacles = 64;
+constexpr int kClusterObstaclesPerGroup = 16;  // C5: 16 workgroups (8..32 measured within 4 %)
+constexpr int kClusterMax = 32;
+#ifndef DRCVAR_CLUSTER_BLOCK
+#define DRCVAR_CLUSTER_BLOCK 512
+#endif
+constexpr int kClusterBlock = DRCVAR_CLUSTER_BLOCK;  // threads per workgroup of the clustered form
+constexpr int kClusterCUs = 256;  // workspace sizing; launches use the device's own CU count
+constexpr int kRec = 512;                        // doubles per exchange record
+constexpr int kRecScalars = kPerStepQ * 64;      // [kPerStepQ][64] per-step sums, then scalars
+constexpr int kRecDigest = kRecScalars + 8;      // the publishing workgroup's state digest
+constexpr int kCtrlDoubles = 16;                 // 128-B control block per problem (the counter)
+constexpr int kClusterScratch = kMaxWaves * 4 + 8;  // LDS doubles of the exchange
+constexpr int kCxGaveUp = kMaxWaves * 4, kCxScalars = kMaxWaves * 4 + 1, kCxDiverged = kMaxWaves * 4 + 5;
+static_assert(kCxDiverged < kClusterScratch, "exchange scratch");
+constexpr unsigned long long kAbortBias = 1ull << 40;
+constexpr int kDefaultSpinUs = 10000;            // 10 ms: a C5 solve is ~1 ms
+enum { kOpSum = 0, kOpMax = 1, kOpMin = 2 };
+// exchange sites (mixed into the published digest)
+enum { kSiteStart = 1, kSiteP1, kSiteP23, kSiteP4, kSitePolishHess, kSitePolishRhs, kSitePolishEq,
+       kSitePolishSign, kSitePolishBad, kSiteFinal };
+
+#ifdef DRCVAR_MPC_STAMPS
+// diagnostic build only: per-category shader-clock totals of problem 0..kStampProblems-1
+constexpr int kStampProblems = 64, kStampSlots = 20;
+__device__ unsigned long long g_mpc_stamps[kStampProblems * kStampSlots];
+__device__ unsigned long long g_cl_stamps[8];  // cluster exchange sub-phases, problem 0, group 0
+#define CL_STAMP(k)                                                     \
+  do {                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                          \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+      g_cl_stamps[(k)] += now_ - cl_t0;                                 \
+      cl_t0 = now_;                                                     \
+    }                                                                   \
+  } while (0)
+#define MPC_PHASE(k)                                                    \
+  do {                                                                  \
+    if (threadIdx.x == 0) {                                             \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+      stamp_acc[(k)] += now_ - stamp_last;                              \
+      stamp_last = now_;                                                \
+    }                                                                   \
+  } while (0)
+#else
+#define CL_STAMP(k) \
+  do {              \
+  } while (0)
+#define MPC_PHASE(k) \
+  do {               \
+  } while (0)
+#endif
+
+#if DRCVAR_MPC_ANY_DEVICE_PART
 // LDS arrays (doubles); offsets from LdsPlan below.
 struct Lds {
   double* Am;     // [nx][kMx] A          (model, copied from the blob at setup)
@@ -1151,30 +1207,20 @@ __device__ __forceinline__ double step_total(const double* red, int q, int lane)
 //   agent-scope loads until all `size` workgroups have arrived at this exchange, then every wave
 //   reads the records with agent-scope loads (they bypass the CU's L1).  Records alternate
 //   between two buffers: a workgroup can be at most one exchange ahead of the slowest reader.
-// Every spin is bounded (kSpinTicks of the 100 MHz clock); a workgroup that gives up adds
-// kAbortBias to the counter, which releases every wait of every workgroup at once, and the
-// problem ends NUMERICAL (the fallback rollout) instead of hanging the launch.  The counters are
-// zeroed by a one-wave kernel in front of every launch; the clustered launch never has more workgroups
-// than the device has CUs, and asks for more LDS than two workgroups can share, so each
-// workgroup has a CU of its own and all of them are resident.
+// Every spin is bounded (MpcArgs::spin_ticks of the 100 MHz clock, default 10 ms); a workgroup
+// that gives up adds kAbortBias to the counter, which releases every wait of every workgroup at
+// once, and the problem ends CLUSTER_TIMEOUT (the fallback rollout) instead of hanging the launch.
+// Divergence check: the protocol's liveness and the answer rest on every workgroup taking the same
+// decisions (they are replicated, bitwise).  Each workgroup folds every replicated decision scalar
+// (merit, step lengths, centring, polish residuals, factorisation outcomes) into a running 64-bit
+// digest and publishes it, mixed with the exchange's site id and epoch, in its record; the gather
+// compares every record's digest with its own.  A mismatch ends the problem at that exchange with
+// CLUSTER_DIVERGED (and the abort bias releases any workgroup waiting elsewhere), instead of
+// combining records from different sites or spinning until the time limit.  The counters are
+// zeroed by a one-wave kernel in front of every launch; the clustered launch never has more
+// workgroups than half the device's CUs, and asks for more LDS than two workgroups can share, so
+// each workgroup has a CU of its own.
 using gu64 = __attribute__((address_space(1))) unsigned long long;
-constexpr int kClusterMaxProblems = 8;
-constexpr int kClusterMinObstacles = 64;
-constexpr int kClusterObstaclesPerGroup = 16;  // C5: 16 workgroups (8..32 measured within 4 %)
-constexpr int kClusterMax = 32;
-#ifndef DRCVAR_CLUSTER_BLOCK
-#define DRCVAR_CLUSTER_BLOCK 512
-#endif
-constexpr int kClusterBlock = DRCVAR_CLUSTER_BLOCK;  // threads per workgroup of the clustered form
-constexpr int kClusterCUs = 256;  // workspace sizing; launches use the device's own CU count
-constexpr int kRec = 512;                        // doubles per exchange record
-constexpr int kRecScalars = kPerStepQ * 64;      // [kPerStepQ][64] per-step sums, then scalars
-constexpr int kCtrlDoubles = 16;                 // 128-B control block per problem (the counter)
-constexpr int kClusterScratch = kMaxWaves * 4 + 8;  // LDS doubles of the exchange
-constexpr unsigned long long kAbortBias = 1ull << 40;
-constexpr uint64_t kSpinTicks = 5000000;         // 50 ms of s_memrealtime (100 MHz)
-enum { kOpSum = 0, kOpMax = 1, kOpMin = 2 };
-
 __device__ __forceinline__ double op_apply(int op, double a, double b) {
   return op == kOpSum ? a + b : (op == kOpMax ? fmax(a, b) : fmin(a, b));
 }
@@ -1192,24 +1238,37 @@ __device__ __forceinline__ double load_wt(const double* p) {  // agent-scope loa
   return __longlong_as_double(static_cast<long long>(
       __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
 }
+// 64-bit mix of a decision into a digest (xor-multiply, FNV-style); the operands are uniform
+__device__ __forceinline__ uint64_t digest_mix(uint64_t d, uint64_t v) {
+  d ^= v + 0x9e3779b97f4a7c15ull + (d << 6) + (d >> 2);
+  return d * 0x100000001b3ull;
+}
 
 struct Cluster {
   int size, id;     // workgroups per problem, this workgroup's index in its cluster
   gu64* ctr;        // the problem's arrival counter
   double* xbuf;     // [2][size][kRec] exchange records
   double* cx;       // LDS scratch [kClusterScratch]
+  uint64_t spin;    // wait bound (100 MHz ticks)
+  uint64_t digest;  // running digest of every replicated decision (uniform in the workgroup)
   unsigned epoch;   // exchanges completed (the same count in every workgroup of the cluster)
-  bool aborted;     // a wait gave up (uniform after the exchange that saw it)
+  bool aborted;     // a wait gave up or the digests disagreed (uniform after that exchange)
+  bool diverged;    // ... the digests disagreed
+  __device__ __forceinline__ void note(double v) {
+    digest = digest_mix(digest, static_cast<uint64_t>(__double_as_longlong(v)));
+  }
+  __device__ __forceinline__ void note_int(int64_t v) { digest = digest_mix(digest, static_cast<uint64_t>(v)); }
 };
 
 // Per-step values acc[q] (lane = step, this thread's rows) combined over the cluster with
 // step_op, and NS scalars sv[i] with ops[i]; on return s.red[q * 64 + lane] holds the cluster's
 // per-step totals and sv[i] the cluster's scalar totals (in every thread).  A sum counts every
 // thread's value once: callers pass row contributions only (max / min may include replicated
-// terms).  Contains barriers: every thread of the workgroup calls it.
+// terms).  `site` names the call site (digest).  Contains barriers: every thread of the workgroup
+// calls it.  After an abort (cl.aborted) the records it returns are not to be used.
 template <int kWaves, int Q, int NS>
 __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* acc, int step_op,
-                                       double* sv, const int* ops) {
+                                       double* sv, const int* ops, int site) {
   static_assert(Q <= kPerStepQ && NS <= 4, "exchange layout");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* cx = cl.cx;
@@ -1226,16 +1285,17 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   __syncthreads();
   CL_STAMP(0);  // partials into LDS + barrier
   const int64_t half = static_cast<int64_t>(cl.epoch & 1u) * cl.size * kRec;
+  const uint64_t mydig = digest_mix(digest_mix(cl.digest, static_cast<uint64_t>(site)), cl.epoch);
   // publish: wave q stores this workgroup's total of quantity q (waves combined in order), the
-  // last wave the scalars; every storing wave drains its stores before the barrier behind which
-  // one lane signals the arrival for all of them
+  // last wave the scalars and the digest; every storing wave drains its stores before the barrier
+  // behind which one lane signals the arrival for all of them
   double* rec = cl.xbuf + half + static_cast<int64_t>(cl.id) * kRec;
   for (int q = wave; q < Q; q += kWaves) {
     double t = s.red[q * 64 + lane];
     for (int w = 1; w < kWaves; ++w) t = op_apply(step_op, t, s.red[(w * kPerStepQ + q) * 64 + lane]);
     store_wt(rec + q * 64 + lane, t);
   }
-  if (NS > 0 && wave == kWaves - 1) {
+  if (wave == kWaves - 1) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       if (lane == i) {
@@ -1244,6 +1304,7 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
         store_wt(rec + kRecScalars + i, t);
       }
     }
+    if (lane == 8) store_wt(rec + kRecDigest, __longlong_as_double(static_cast<long long>(mydig)));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the record is out before the arrival
   CL_STAMP(1);  // combine over waves + record stores drained
@@ -1264,7 +1325,7 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
         gave_up = v >= kAbortBias;
         break;
       }
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {  // bounded: release everyone
+      if (__builtin_amdgcn_s_memrealtime() - t0 > cl.spin) {  // bounded: release everyone
         if (lane == 0) __hip_atomic_fetch_add(cl.ctr, kAbortBias, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gave_up = true;
         break;
@@ -1272,15 +1333,15 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
       __builtin_amdgcn_s_sleep(1);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
-    if (lane == 0) cx[kMaxWaves * 4] = gave_up ? 1.0 : 0.0;
+    if (lane == 0) cx[kCxGaveUp] = gave_up ? 1.0 : 0.0;
     CL_STAMP(3);  // arrival + poll (includes waiting for the slowest workgroup)
   }
   __syncthreads();
   CL_STAMP(4);  // barrier after the poll
   // Gather: wave q sums quantity q (lane = step) over the records in workgroup order, eight
   // agent-scope loads in flight at a time — the same order in every workgroup of the cluster; the
-  // last wave gathers the scalars (lane = record).  (16-B loads of step pairs, two halves of the
-  // records per wave, measured slower: the extra live registers spilled.)
+  // last wave gathers the scalars and checks the digests (lane = record).  (16-B loads of step
+  // pairs, two halves of the records per wave, measured slower: the extra live registers spilled.)
   const double* base = cl.xbuf + half;
   for (int q = wave; q < Q; q += kWaves) {
     double v[8];
@@ -1295,20 +1356,28 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
     }
     s.red[q * 64 + lane] = t;
   }
-  if (NS > 0 && wave == kWaves - 1) {
+  if (wave == kWaves - 1) {
+    const double* rl = base + static_cast<int64_t>(lane < cl.size ? lane : 0) * kRec;
+    const uint64_t dg = static_cast<uint64_t>(__double_as_longlong(load_wt(rl + kRecDigest)));
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      double v = lane < cl.size ? load_wt(base + static_cast<int64_t>(lane) * kRec + kRecScalars + i)
-                                : op_identity(ops[i]);
+      double v = lane < cl.size ? load_wt(rl + kRecScalars + i) : op_identity(ops[i]);
       v = op_wave(ops[i], v);
-      if (lane == 0) cx[kMaxWaves * 4 + 1 + i] = v;
+      if (lane == 0) cx[kCxScalars + i] = v;
     }
+    // (after a wait gave up the records are incomplete: no digest verdict on them)
+    const bool differs = cx[kCxGaveUp] == 0.0 && __ballot(lane < cl.size && dg != mydig) != 0ull;
+    if (differs && lane == 0)  // release whoever waits at another exchange
+      __hip_atomic_fetch_add(cl.ctr, kAbortBias, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) cx[kCxDiverged] = differs ? 1.0 : 0.0;
   }
   __syncthreads();
   CL_STAMP(5);  // records gathered and combined
 #pragma unroll
-  for (int i = 0; i < NS; ++i) sv[i] = cx[kMaxWaves * 4 + 1 + i];
-  cl.aborted = cl.aborted || cx[kMaxWaves * 4] != 0.0;
+  for (int i = 0; i < NS; ++i) sv[i] = cx[kCxScalars + i];
+  const bool div = cx[kCxDiverged] != 0.0;
+  cl.diverged = cl.diverged || (div && !cl.aborted);
+  cl.aborted = cl.aborted || div || cx[kCxGaveUp] != 0.0;
   ++cl.epoch;
 }
 
@@ -1334,6 +1403,12 @@ constexpr int kSweep = 1;
 #define ROW_SWEEP_END \
   }                   \
   }
+
+// fold a replicated decision scalar into the cluster's digest (clustered form only)
+#define CL_NOTE(x)                \
+  do {                            \
+    if constexpr (CL) cl.note(x); \
+  } while (0)
 
 // BLK threads per problem; HMX the horizon capacity of its LDS plan.  Every form targets two
 // waves per SIMD (HIP's second launch bound; VGPR budget 256): 512 and 256 threads with two
@@ -1363,8 +1438,11 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     cl.ctr = (gu64*)(a.ws + b * kCtrlDoubles);
     cl.xbuf = ws + kRowArrays * static_cast<int64_t>(O) * kStepPad + static_cast<int64_t>(cl_size) * kBestPad;
     cl.cx = lds_raw + LdsPlan<kWaves, NU, NX, HMX>::total;
+    cl.spin = a.spin_ticks;
+    cl.digest = 0;
     cl.epoch = 0;
     cl.aborted = false;
+    cl.diverged = false;
   }
   (void)cl;
   (void)O;
@@ -1470,7 +1548,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   if constexpr (CL) {  // |g| over every workgroup's rows (the bound terms are replicated: max)
     const int ops[1] = {kOpMax};
     MPC_PHASE(0);
-    cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &gmax, ops);
+    cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &gmax, ops, kSiteStart);
     MPC_PHASE(16);  // cluster exchange
   }
   {
@@ -1551,8 +1629,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         double sv[3] = {gap_rows, rpm_rows, rdm_rows};
         const int ops[3] = {kOpSum, kOpMax, kOpMax};
         MPC_PHASE(1);
-        cluster_combine<kWaves, kPerStepQ, 3>(cl, s, acc, kOpSum, sv, ops);
+        cluster_combine<kWaves, kPerStepQ, 3>(cl, s, acc, kOpSum, sv, ops, kSiteP1);
         MPC_PHASE(16);  // cluster exchange
+        if (cl.aborted) break;  // uniform: the cluster disagreed or a wait gave up
         gap = tid == 0 ? sv[0] : 0.0;
         rpm = sv[1];
         rdm = sv[2];
@@ -1620,6 +1699,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         break;
       }
       const double merit = fmax(fmax(rp / scale_d, rd / scale_q), mu);
+      CL_NOTE(merit);
       if (merit <= tol_r) {
         status = DRCVAR_MPC_STATUS_OPTIMAL;
         best_merit = merit;
@@ -1648,6 +1728,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
+    CL_NOTE(s.Ri[0]);  // the factorisation (its first pivot's inverse)
     MPC_PHASE(3);
     newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa);  // direction and its positions
     MPC_PHASE(4);
@@ -1685,8 +1766,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         double sv[4] = {amax, gq0, gq1, gq2};
         const int ops[4] = {kOpMin, kOpSum, kOpSum, kOpSum};
         MPC_PHASE(5);
-        cluster_combine<kWaves, 4, 4>(cl, s, acc, kOpSum, sv, ops);
+        cluster_combine<kWaves, 4, 4>(cl, s, acc, kOpSum, sv, ops, kSiteP23);
         MPC_PHASE(16);  // cluster exchange
+        if (cl.aborted) break;
         amax = sv[0];
         gq0 = tid == 0 ? sv[1] : 0.0;  // the quadratic enters the block sum once
         gq1 = tid == 0 ? sv[2] : 0.0;
@@ -1758,6 +1840,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       gap_aff = block_sum<kWaves>(gap_aff, s.sc);  // its barriers also publish za / zu / rU / rUu
       const double ratio_g = gap > 0.0 ? gap_aff / gap : 0.0;
       const double sigma_mu = ratio_g * ratio_g * ratio_g * mu;
+      CL_NOTE(a_aff);
+      CL_NOTE(sigma_mu);
       s.sc[63] = sigma_mu;  // same value in every thread; kept for P4/P5
       // Gp' is linear: Gp' za + sigma_mu Gp' zu = Gp' (za + sigma_mu zu), combined in place
       for (int t = tid; t < 2 * H; t += kBlock) s.zu[t] = s.za[t] + sigma_mu * s.zu[t];
@@ -1787,8 +1871,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     if constexpr (CL) {
       const int ops[1] = {kOpMin};
       MPC_PHASE(5);
-      cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &amax, ops);
+      cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &amax, ops, kSiteP4);
       MPC_PHASE(16);  // cluster exchange
+      if (cl.aborted) break;
     }
     if (a.has_u) {
       for (int j = tid; j < n; j += kBlock) {
@@ -1808,7 +1893,11 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     // fraction to the boundary: 0.995, closing to 1 - mu near the solution — a fixed 0.995 caps
     // the tail at a factor-200 reduction per iteration (measured 6e-2, 3e-4, 2e-6, 8e-9, 4e-11)
-    const double alpha = fmin(1.0, (1.0 - fmin(1.0 - kStepFrac, mu)) * block_min<kWaves>(amax, s.sc));
+    double alpha = fmin(1.0, (1.0 - fmin(1.0 - kStepFrac, mu)) * block_min<kWaves>(amax, s.sc));
+    if constexpr (CL) {
+      if (a.perturb_group == cid + 1 && it == a.perturb_iter) alpha *= 1.0 - 0x1p-20;  // test hook
+      cl.note(alpha);
+    }
 
     // ---- P5: update (the halfspace rows in the fused pass below) ----
     // this lane's step: positions and directions of the iterate being updated
@@ -1891,7 +1980,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // reuse the Hessian assembly, the Cholesky and the triangular solves), and rows whose sign
   // conditions fail are moved (primal-dual active-set step), up to kPolishAttempts times.  On
   // success the answer is exact to roundoff; otherwise the interior-point answer stands.
-  const bool tried = a.polish && best_merit <= kPolishMerit;
+  const bool tried = a.polish && best_merit <= kPolishMerit && !(CL && cl.aborted);
   if (tried) {
     for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];  // the answer if polishing fails
     // classify: flag 0 = halfspace not binding (s = 0), 1 = slack positive (s = h.p + g > 0),
@@ -1934,7 +2023,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     __syncthreads();
     const double tolf = 1e-9 * scale_d;
-    for (int attempt = 0; attempt < kPolishAttempts && !polished; ++attempt) {
+    for (int attempt = 0; attempt < kPolishAttempts && !polished && !(CL && cl.aborted); ++attempt) {
       // test hook; a loop bound computed from it instead (attempts = hook ? 0 : kPolishAttempts)
       // broke the 4-input kernels' polish (8 % polished) — a codegen effect, not a semantic one
       if (round == 0 && a.force_resume) break;
@@ -1955,8 +2044,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
         if constexpr (CL) {
           MPC_PHASE(10);
-          cluster_combine<kWaves, 3, 0>(cl, s, acc, kOpSum, nullptr, nullptr);
+          cluster_combine<kWaves, 3, 0>(cl, s, acc, kOpSum, nullptr, nullptr, kSitePolishHess);
           MPC_PHASE(16);  // cluster exchange
+          if (cl.aborted) break;
         } else {
 #pragma unroll
           for (int q = 0; q < 3; ++q) s.red[(wave * kPerStepQ + q) * 64 + lane] = acc[q];
@@ -1980,6 +2070,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       }
       MPC_PHASE(10);
       if (!riccati_factor<NU, NX>(s, H) && !riccati_factor<NU, NX, true>(s, H)) break;
+      CL_NOTE(s.Ri[0]);
       MPC_PHASE(11);
       for (int pass = 0; pass < kPolishIters; ++pass) {
         // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
@@ -1999,8 +2090,9 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
         if constexpr (CL) {
           MPC_PHASE(12);
-          cluster_combine<kWaves, 2, 0>(cl, s, acc, kOpSum, nullptr, nullptr);
+          cluster_combine<kWaves, 2, 0>(cl, s, acc, kOpSum, nullptr, nullptr, kSitePolishRhs);
           MPC_PHASE(16);  // cluster exchange
+          if (cl.aborted) break;
         } else {
           s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];
           s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
@@ -2080,11 +2172,12 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         if constexpr (CL) {  // every workgroup's equality rows (the bound terms: replicated)
           const int ops[1] = {kOpMax};
           MPC_PHASE(12);
-          cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &eres, ops);
+          cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &eres, ops, kSitePolishEq);
           MPC_PHASE(16);  // cluster exchange
         }
         double unused_a = 0.0, unused_b = 0.0;
         block_sum_max_max<kWaves>(unused_a, eres, unused_b, s.sc);  // uniform; also the barrier
+        CL_NOTE(eres);
         if (eres <= kPolishEqTol * scale_d) break;
       }
       // sign conditions; violators move (primal-dual active-set step).  Rows that must become
@@ -2109,7 +2202,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         if constexpr (CL) {  // per-step maxima over the cluster's rows
           const double vm[2] = {vmax, dmax};
           MPC_PHASE(7);
-          cluster_combine<kWaves, 2, 0>(cl, s, vm, kOpMax, nullptr, nullptr);
+          cluster_combine<kWaves, 2, 0>(cl, s, vm, kOpMax, nullptr, nullptr, kSitePolishSign);
           MPC_PHASE(16);  // cluster exchange
         } else {
           s.red[(wave * kPerStepQ) * 64 + lane] = vmax;
@@ -2159,7 +2252,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       if constexpr (CL) {  // unresolved rows of the whole cluster, counted once (thread 0)
         const int ops[1] = {kOpSum};
         MPC_PHASE(7);
-        cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &bad, ops);
+        cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &bad, ops, kSitePolishBad);
         MPC_PHASE(16);  // cluster exchange
         bad = tid == 0 ? bad : 0.0;
       }
@@ -2192,6 +2285,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
       }
       bad = block_sum<kWaves>(bad, s.sc);
+      CL_NOTE(bad);
       if (bad == 0.0) polished = true;
     }
     if (polished) {
@@ -2228,38 +2322,45 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
 
   MPC_PHASE(7);
   // ------------------------------- output -------------------------------
+  // A cluster that disagreed or whose wait gave up rolls the fallback inputs out, like any failed
+  // solve (core/mpc_filter.py:166-178), with a status of its own.
+  const int abort_status = CL && cl.diverged ? DRCVAR_MPC_STATUS_CLUSTER_DIVERGED : DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT;
   if constexpr (CL) {
-    if (cl.aborted) status = DRCVAR_MPC_STATUS_NUMERICAL;  // a cluster wait gave up: fallback
+    if (cl.aborted) status = abort_status;
   }
-  const bool optimal = status == DRCVAR_MPC_STATUS_OPTIMAL || status == DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
-  if (!optimal) {
-    const double* uf = a.uf + b * a.uf_sp;
-    for (int j = tid; j < n; j += kBlock) s.u[j] = uf[(j / NU) * a.uf_st + j % NU];
-  }
-  for (int q = tid; q < nx; q += kBlock) s.xs[q] = x0[q];
-  __syncthreads();
-  positions<NU, kBlock>(s, s.u, s.p, s.c, H);  // positions of the returned inputs (slacks below)
-  // x_{t+1} = A x_t + B u_t (core/mpc_filter.py:85-86, :216-217): wave 0, lane q < nx holds x_q,
-  // the state moving between lanes by readlane — no barrier per step
-  if (tid < 64) {
-    const int li = lane < nx ? lane : 0;
-    double Arow[NX], Brow[NU];
-#pragma unroll
-    for (int m = 0; m < NX; ++m) Arow[m] = s.Am[li * kMx + m];  // zero-padded beyond nx
-#pragma unroll
-    for (int c = 0; c < NU; ++c) Brow[c] = s.Bm[li * NU + c];
-    double xv = lane < nx ? x0[lane] : 0.0;
-    for (int t = 0; t < H; ++t) {
-      double acc = 0.0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) acc += Arow[m] * readlane_f64(xv, m);
-#pragma unroll
-      for (int c = 0; c < NU; ++c) acc += Brow[c] * s.u[t * NU + c];
-      xv = lane < nx ? acc : 0.0;
-      if (lane < nx) s.xs[(t + 1) * nx + lane] = acc;
+  bool optimal = status == DRCVAR_MPC_STATUS_OPTIMAL || status == DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
+  // the returned inputs (the fallback's unless optimal), their positions and states
+  auto rollout = [&]() __attribute__((always_inline)) {
+    if (!optimal) {
+      const double* uf = a.uf + b * a.uf_sp;
+      for (int j = tid; j < n; j += kBlock) s.u[j] = uf[(j / NU) * a.uf_st + j % NU];
     }
-  }
-  __syncthreads();
+    for (int q = tid; q < nx; q += kBlock) s.xs[q] = x0[q];
+    __syncthreads();
+    positions<NU, kBlock>(s, s.u, s.p, s.c, H);  // positions of the returned inputs (slacks below)
+    // x_{t+1} = A x_t + B u_t (core/mpc_filter.py:85-86, :216-217): wave 0, lane q < nx holds x_q,
+    // the state moving between lanes by readlane — no barrier per step
+    if (tid < 64) {
+      const int li = lane < nx ? lane : 0;
+      double Arow[NX], Brow[NU];
+#pragma unroll
+      for (int m = 0; m < NX; ++m) Arow[m] = s.Am[li * kMx + m];  // zero-padded beyond nx
+#pragma unroll
+      for (int c = 0; c < NU; ++c) Brow[c] = s.Bm[li * NU + c];
+      double xv = lane < nx ? x0[lane] : 0.0;
+      for (int t = 0; t < H; ++t) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc += Arow[m] * readlane_f64(xv, m);
+#pragma unroll
+        for (int c = 0; c < NU; ++c) acc += Brow[c] * s.u[t * NU + c];
+        xv = lane < nx ? acc : 0.0;
+        if (lane < nx) s.xs[(t + 1) * nx + lane] = acc;
+      }
+    }
+    __syncthreads();
+  };
+  rollout();
   // objective (core/mpc_filter.py:64-76,142-144) and the largest slack
   double obj = 0.0, smax = 0.0, obj_rows = 0.0;
   double& obj_hs = CL ? obj_rows : obj;  // the rows' terms (clustered: summed over the cluster)
@@ -2293,14 +2394,19 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
   }
   if constexpr (CL) {
+    if (a.stall_group == cid + 1) return;  // test hook: never arrives at the final exchange
     double sv[2] = {obj_rows, smax};
     const int ops[2] = {kOpSum, kOpMax};
     MPC_PHASE(8);
-    cluster_combine<kWaves, 0, 2>(cl, s, nullptr, kOpSum, sv, ops);
+    cluster_combine<kWaves, 0, 2>(cl, s, nullptr, kOpSum, sv, ops, kSiteFinal);
     MPC_PHASE(16);  // cluster exchange
     obj += tid == 0 ? sv[0] : 0.0;
     smax = sv[1];
-    if (cl.aborted) status = DRCVAR_MPC_STATUS_NUMERICAL;
+    if (cl.aborted && optimal) {  // this exchange gave up: the fallback after all
+      status = cl.diverged ? DRCVAR_MPC_STATUS_CLUSTER_DIVERGED : DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT;
+      optimal = false;
+      rollout();
+    }
     if (cid != 0) return;  // workgroup 0 writes the problem's outputs (every one holds them)
   }
   double unused = 0.0;
@@ -2331,54 +2437,10 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
 #endif
 }
 
-// ------------------------------- host side -------------------------------
-
-bool all_finite(const double* p, int64_t n) {
-  for (int64_t i = 0; i < n; ++i)
-    if (!std::isfinite(p[i])) return false;
-  return true;
-}
-
-// Clustered launches (a few large problems): workgroups per problem.  Two obstacles per wave of
-// the 512-thread form (16 per workgroup), at most kClusterMax workgroups per problem
-// and never more workgroups in all than CUs.  Problems with fewer than kClusterMinObstacles
-// obstacles (≤ 8 rows per thread on one workgroup) stay on one workgroup: the exchanges
-// (~3 per interior-point iteration) would cost more than the sweeps they split (constants
-// kCluster* with the exchange layout above).
-// the most workgroups a problem of this batch may use (1: not eligible for the clustered form)
-int cluster_limit(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
-  if (n_problems < 1 || n_problems > kClusterMaxProblems || n_obstacles < kClusterMinObstacles) return 1;
-  int64_t c = n_obstacles < kClusterMax ? n_obstacles : kClusterMax;
-  c = c < cus / n_problems ? c : cus / n_problems;
-  return c < 2 ? 1 : static_cast<int>(c);
-}
-
-// the workgroups a launch uses: kClusterObstaclesPerGroup obstacles each, or the
-// DRCVAR_MPC_CLUSTER=<c> override (A/B runs; 1 = the one-workgroup form), within the limit
-int cluster_size(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
-  const int lim = cluster_limit(n_problems, n_obstacles, cus);
-  if (lim == 1) return 1;
-  int64_t c = (n_obstacles + kClusterObstaclesPerGroup - 1) / kClusterObstaclesPerGroup;
-  const char* e = std::getenv("DRCVAR_MPC_CLUSTER");
-  if (e && *e) c = std::atoi(e);
-  c = c < lim ? c : lim;
-  return c < 2 ? 1 : static_cast<int>(c);
-}
-
 // zeroes the per-problem arrival counters of a clustered launch (in front of it, same stream)
 __global__ void zero_counters_kernel(double* ws, int n_problems) {
   for (int b = threadIdx.x; b < n_problems; b += blockDim.x)
     __hip_atomic_store((gu64*)(ws + b * kCtrlDoubles), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-int device_cus() {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  static int cached[64] = {};
-  if (dev >= 0 && dev < 64 && cached[dev] > 0) return cached[dev];
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (dev >= 0 && dev < 64) cached[dev] = cus;
-  return cus;
 }
 
 template <int NU, int NX, int BLK, int HMX = DRCVAR_MPC_MAX_HORIZON, bool CL = false>
@@ -2427,11 +2489,79 @@ int launch_nu(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
                        : launch<NU, 8, 256>(args, n_problems, stream);
 }
 
+#endif  // DRCVAR_MPC_ANY_DEVICE_PART
+
+#if DRCVAR_MPC_HOST_PART
+// ------------------------------- host side -------------------------------
+
+bool all_finite(const double* p, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (!std::isfinite(p[i])) return false;
+  return true;
+}
+
+// Clustered launches (a few large problems): workgroups per problem.  Two obstacles per wave of
+// the 512-thread form (16 per workgroup), at most kClusterMax workgroups per problem
+// and never more workgroups in all than half the CUs (the workspace is sized for all of them).
+// Problems with fewer than kClusterMinObstacles
+// obstacles (≤ 8 rows per thread on one workgroup) stay on one workgroup: the exchanges
+// (~3 per interior-point iteration) would cost more than the sweeps they split (constants
+// kCluster* with the exchange layout above).
+// the most workgroups a problem of this batch may use (1: not eligible for the clustered form)
+int cluster_limit(int64_t n_problems, int64_t n_obstacles, int64_t cus) {
+  if (n_problems < 1 || n_problems > kClusterMaxProblems || n_obstacles < kClusterMinObstacles) return 1;
+  int64_t c = n_obstacles < kClusterMax ? n_obstacles : kClusterMax;
+  c = c < cus / n_problems ? c : cus / n_problems;
+  return c < 2 ? 1 : static_cast<int>(c);
+}
+
+// the workgroups a launch uses: kClusterObstaclesPerGroup obstacles each, or `requested` (> 0:
+// drcvar_mpc_options.cluster_size, A/B runs and tests; 1 = the one-workgroup form), within the
+// limit for half the device's CUs: a clustered launch's workgroups must all be resident at once,
+// and half the chip leaves room for whatever else runs beside it (another stream, another process)
+int cluster_size(int64_t n_problems, int64_t n_obstacles, int64_t cus, int requested) {
+  const int lim = cluster_limit(n_problems, n_obstacles, cus / 2);
+  if (lim == 1) return 1;
+  int64_t c = (n_obstacles + kClusterObstaclesPerGroup - 1) / kClusterObstaclesPerGroup;
+  if (requested > 0) c = requested;
+  c = c < lim ? c : lim;
+  return c < 2 ? 1 : static_cast<int>(c);
+}
+
+#endif  // DRCVAR_MPC_HOST_PART
 }  // namespace
 
+namespace drcvar_mpc_detail {
+#if DRCVAR_MPC_DEVICE_PART(1)
+int launch_nu1(const MpcArgs& args, int64_t n_problems, hipStream_t stream) { return launch_nu<1>(args, n_problems, stream); }
+#endif
+#if DRCVAR_MPC_DEVICE_PART(2)
+int launch_nu2(const MpcArgs& args, int64_t n_problems, hipStream_t stream) { return launch_nu<2>(args, n_problems, stream); }
+#endif
+#if DRCVAR_MPC_DEVICE_PART(3)
+int launch_nu3(const MpcArgs& args, int64_t n_problems, hipStream_t stream) { return launch_nu<3>(args, n_problems, stream); }
+#endif
+#if DRCVAR_MPC_DEVICE_PART(4)
+int launch_nu4(const MpcArgs& args, int64_t n_problems, hipStream_t stream) { return launch_nu<4>(args, n_problems, stream); }
+#endif
+#if DRCVAR_MPC_HOST_PART
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  static int cached[64] = {};
+  if (dev >= 0 && dev < 64 && cached[dev] > 0) return cached[dev];
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (dev >= 0 && dev < 64) cached[dev] = cus;
+  return cus;
+}
+
+#endif
+}  // namespace drcvar_mpc_detail
+
+#if DRCVAR_MPC_HOST_PART
 extern "C" {
 
-#ifdef DRCVAR_MPC_STAMPS
+#if defined(DRCVAR_MPC_STAMPS) && !defined(DRCVAR_MPC_PART)
 // diagnostic build only (not part of the ABI header)
 int drcvar_diag_cluster_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cl_stamps), sizeof(g_cl_stamps), 0,
@@ -2574,26 +2704,37 @@ int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_pr
                        static_cast<int64_t>(c) * (kBestPad + 2 * kRec));
 }
 
-int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,
-                                 int64_t n_obstacles) {
+int32_t drcvar_mpc_launch_groups_ex(const drcvar_mpc_model* model, int64_t n_problems,
+                                    int64_t n_obstacles, const drcvar_mpc_options* options) {
   if (!model || n_problems < 0 || n_obstacles < 0) return -1;
+  if (options && options->cluster_size < 0) return -1;
   if (cluster_limit(n_problems, n_obstacles, kClusterCUs) == 1) return 1;
   const int cus = device_cus();
-  const int c = cluster_size(n_problems, n_obstacles, cus > 0 ? cus : 1);
+  const int c = cluster_size(n_problems, n_obstacles, cus > 0 ? cus : 1, options ? options->cluster_size : 0);
   const int c_ws = cluster_limit(n_problems, n_obstacles, kClusterCUs);  // what the workspace holds
   return c < c_ws ? c : c_ws;
 }
 
-int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
-                          const double* hs_h, const double* hs_g, int64_t n_obstacles,
-                          int64_t n_hs_steps, int64_t h_sp, int64_t h_so, int64_t h_sk,
-                          int64_t g_sp, int64_t g_so, int64_t g_sk, const double* x0,
-                          int64_t x0_sp, const double* x_ref, int64_t xr_sp, int64_t xr_st,
-                          const double* u_fallback, int64_t uf_sp, int64_t uf_st, int32_t max_iter,
-                          double tol, int32_t polish, double* x_out, double* u_out, double* info_out,
-                          double* workspace, int64_t workspace_doubles, void* stream) {
+int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,
+                                 int64_t n_obstacles) {
+  return drcvar_mpc_launch_groups_ex(model, n_problems, n_obstacles, nullptr);
+}
+
+int drcvar_mpc_filter_f64_ex(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
+                             const double* hs_h, const double* hs_g, int64_t n_obstacles,
+                             int64_t n_hs_steps, int64_t h_sp, int64_t h_so, int64_t h_sk,
+                             int64_t g_sp, int64_t g_so, int64_t g_sk, const double* x0,
+                             int64_t x0_sp, const double* x_ref, int64_t xr_sp, int64_t xr_st,
+                             const double* u_fallback, int64_t uf_sp, int64_t uf_st,
+                             int32_t max_iter, double tol, int32_t polish, double* x_out,
+                             double* u_out, double* info_out, double* workspace,
+                             int64_t workspace_doubles, const drcvar_mpc_options* options,
+                             void* stream) {
   if (!model || !blob || n_problems < 0 || n_obstacles < 0 || n_hs_steps < 0)
     return DRCVAR_ERR_INVALID_ARGUMENT;
+  drcvar_mpc_options opt{};
+  if (options) opt = *options;
+  if (opt.cluster_size < 0 || opt.spin_limit_us < 0) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (n_problems == 0) return DRCVAR_OK;
   if (!x0 || !x_ref || !u_fallback || !x_out || !u_out || !info_out) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (max_iter < 1 || !(tol > 0.0) || n_problems > 0x7fffffffLL) return DRCVAR_ERR_INVALID_ARGUMENT;
@@ -2653,27 +2794,44 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
   if (c_ws > 1) {  // the workspace is laid out for c_ws; a smaller device or the cap uses fewer
     args.ws_off = kCtrlDoubles * n_problems;
     args.ws_pp = kRowArrays * n_obstacles * kStepPad + static_cast<int64_t>(c_ws) * (kBestPad + 2 * kRec);
-    args.cl_size = drcvar_mpc_launch_groups(model, n_problems, n_obstacles);
+    args.cl_size = drcvar_mpc_launch_groups_ex(model, n_problems, n_obstacles, &opt);
   }
   args.max_iter = max_iter;
   args.tol = tol;
   args.polish = polish;
-  {  // test hook: every problem that meets tol takes the resume round (tests/test_mpc_cluster.py)
-    const char* fr = std::getenv("DRCVAR_MPC_FORCE_RESUME");
-    args.force_resume = fr && fr[0] == '1';
-  }
+  args.spin_ticks = static_cast<uint64_t>(opt.spin_limit_us > 0 ? opt.spin_limit_us : kDefaultSpinUs) * 100u;
+  args.force_resume = opt.debug_force_resume != 0;
+  args.perturb_group = opt.debug_perturb_group;
+  args.perturb_iter = opt.debug_perturb_iteration;
+  args.stall_group = opt.debug_stall_group;
 
   (void)hipGetLastError();
   auto st = static_cast<hipStream_t>(stream);
   int rc;
   switch (nu) {
-    case 1: rc = launch_nu<1>(args, n_problems, st); break;
-    case 2: rc = launch_nu<2>(args, n_problems, st); break;
-    case 3: rc = launch_nu<3>(args, n_problems, st); break;
-    default: rc = launch_nu<4>(args, n_problems, st); break;
+    case 1: rc = launch_nu1(args, n_problems, st); break;
+    case 2: rc = launch_nu2(args, n_problems, st); break;
+    case 3: rc = launch_nu3(args, n_problems, st); break;
+    default: rc = launch_nu4(args, n_problems, st); break;
   }
   if (rc != DRCVAR_OK) return rc;
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
 }
 
+int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
+                          const double* hs_h, const double* hs_g, int64_t n_obstacles,
+                          int64_t n_hs_steps, int64_t h_sp, int64_t h_so, int64_t h_sk,
+                          int64_t g_sp, int64_t g_so, int64_t g_sk, const double* x0,
+                          int64_t x0_sp, const double* x_ref, int64_t xr_sp, int64_t xr_st,
+                          const double* u_fallback, int64_t uf_sp, int64_t uf_st, int32_t max_iter,
+                          double tol, int32_t polish, double* x_out, double* u_out, double* info_out,
+                          double* workspace, int64_t workspace_doubles, void* stream) {
+  return drcvar_mpc_filter_f64_ex(model, blob, n_problems, hs_h, hs_g, n_obstacles, n_hs_steps,
+                                  h_sp, h_so, h_sk, g_sp, g_so, g_sk, x0, x0_sp, x_ref, xr_sp,
+                                  xr_st, u_fallback, uf_sp, uf_st, max_iter, tol, polish, x_out,
+                                  u_out, info_out, workspace, workspace_doubles, nullptr, stream);
+}
+
 }  // extern "C"
+
+#endif  // DRCVAR_MPC_HOST_PART

@@ -120,11 +120,19 @@ class PreparedLaunch:
             _native.check(code)
 
 
+def _check_status(status, n, device):
+    if not isinstance(status, torch.Tensor) or status.dtype != torch.int32 or status.device != device \
+            or status.numel() != n or not status.is_contiguous():
+        raise ValueError(f"status must be a contiguous int32 tensor of {n} elements on {device}")
+
+
 def prepare_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams,
                             out: torch.Tensor | None = None, stream=None,
-                            geometry: tuple[int, int] | None = None) -> tuple[PreparedLaunch, torch.Tensor]:
+                            geometry: tuple[int, int] | None = None,
+                            status: torch.Tensor | None = None) -> tuple[PreparedLaunch, torch.Tensor]:
     """Freeze one ``drcvar_safe_halfspaces_f64`` call; ``geometry=(threads, per_thread)`` selects a
-    specific compiled launch geometry through ``drcvar_safe_halfspaces_f64_ex`` (tuning)."""
+    specific compiled launch geometry, ``status`` (int32 ``[O, T]``) receives the per-unit status
+    word (``_native.UNIT_*``) — both through ``drcvar_safe_halfspaces_f64_v2``."""
     params.validate()
     _check_samples(samples, 4)
     O, T, N, _ = samples.shape
@@ -139,31 +147,38 @@ def prepare_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: Ri
             ctypes.c_void_p(ego.data_ptr()), ego.stride(0),
             params.robot_radius, params.obstacle_radius, params.alpha, params.delta, params.epsilon,
             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(_stream_handle(samples.device, stream)))
-    if geometry is not None:
-        geo = tuple(ctypes.c_int32(int(g)) for g in geometry)
-        return PreparedLaunch(lib.drcvar_safe_halfspaces_f64_ex, args + geo, (samples, ego, out)), out
+    if geometry is not None or status is not None:
+        if status is not None:
+            _check_status(status, O * T, samples.device)
+        geo = tuple(ctypes.c_int32(int(g)) for g in (geometry or (0, 0)))
+        st_ptr = ctypes.c_void_p(status.data_ptr() if status is not None else None)
+        args2 = args[:-1] + (st_ptr, args[-1]) + geo
+        return PreparedLaunch(lib.drcvar_safe_halfspaces_f64_v2, args2, (samples, ego, out, status)), out
     return PreparedLaunch(lib.drcvar_safe_halfspaces_f64, args, (samples, ego, out)), out
 
 
 def safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams = RiskParams(),
-                    out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                    out: torch.Tensor | None = None, stream=None,
+                    status: torch.Tensor | None = None) -> torch.Tensor:
     """Mean / CVaR / DR-CVaR halfspaces of every (obstacle, step) unit.
 
     samples [O, T, N, 2] float64 (device), ego [T, 2] float64 (device) -> [O, T, 8] float64 with
-    columns (mean_h0, mean_h1, g_mean, h0, h1, g_cvar, g_dr_star, g_dr_tilde).
+    columns (mean_h0, mean_h1, g_mean, h0, h1, g_cvar, g_dr_star, g_dr_tilde).  ``status``
+    (optional int32 ``[O, T]`` device tensor) receives each unit's ``_native.UNIT_*`` bits.
     """
-    launch, out = prepare_safe_halfspaces(samples, ego, params, out, stream)
+    launch, out = prepare_safe_halfspaces(samples, ego, params, out, stream, status=status)
     if samples.shape[0] * samples.shape[1] > 0:
         launch()
     return out
 
 
 def offsets_given_h(samples: torch.Tensor, h: torch.Tensor, params: RiskParams = RiskParams(),
-                    out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                    out: torch.Tensor | None = None, stream=None,
+                    status: torch.Tensor | None = None) -> torch.Tensor:
     """``cvar_halfspace`` / ``dr_cvar_halfspace`` for U units with given directions.
 
     samples [U, N, 2] float64 (device), h [U, 2] float64 (device) -> [U, 8] float64 (same columns;
-    h echoed in columns 3..4).
+    h echoed in columns 3..4).  ``status`` (optional int32 ``[U]``) receives the ``UNIT_*`` bits.
     """
     params.validate()
     _check_samples(samples, 3)
@@ -173,12 +188,16 @@ def offsets_given_h(samples: torch.Tensor, h: torch.Tensor, params: RiskParams =
         out = torch.empty((U, OUT_WIDTH), dtype=torch.float64, device=samples.device)
     else:
         _check_out(out, (U, OUT_WIDTH), samples.device, "[U, 8]")
+    if status is not None:
+        _check_status(status, U, samples.device)
     if U == 0:
         return out
     lib = _native.lib()
-    _native.check(lib.drcvar_offsets_given_h_f64(
+    _native.check(lib.drcvar_offsets_given_h_f64_v2(
         ctypes.c_void_p(samples.data_ptr()), U, N, samples.stride(0), samples.stride(1),
         ctypes.c_void_p(h.data_ptr()), h.stride(0),
         params.robot_radius, params.obstacle_radius, params.alpha, params.delta, params.epsilon,
-        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(_stream_handle(samples.device, stream))))
+        ctypes.c_void_p(out.data_ptr()),
+        ctypes.c_void_p(status.data_ptr() if status is not None else None),
+        ctypes.c_void_p(_stream_handle(samples.device, stream))))
     return out

@@ -59,7 +59,7 @@ class SafetyFilteringEnvironment:
         """Device-side result: a HalfspaceBatch whose record is [O, T, 8] (T = min(len(ref), H)).
 
         Each unit is solved with the parameters of the reference's optimiser singleton for its N
-        (``risk_metrics.singleton_params`` over the reference's call order: steps outer,
+        (``risk_metrics.plan_singletons`` over the reference's call order: steps outer,
         obstacles inner), so a previous call with the same N but other alpha/delta/epsilon
         carries over exactly as in the reference; usually that is one launch per distinct N.
         """
@@ -75,9 +75,9 @@ class SafetyFilteringEnvironment:
         if n_obstacles == 0 or n_steps == 0:
             return HalfspaceBatch(record)
         counts = [int(np.shape(tr)[0]) for tr in obstacle_sample_trajectories]
-        keys = risk_metrics.singleton_params([counts[o] for _ in range(n_steps)
-                                              for o in range(n_obstacles)],
-                                             self.ALPHA, self.DELTA, self.EPSILON)
+        keys, final = risk_metrics.plan_singletons([counts[o] for _ in range(n_steps)
+                                                    for o in range(n_obstacles)],
+                                                   self.ALPHA, self.DELTA, self.EPSILON)
         groups: dict[int, list[int]] = {}
         for i, n in enumerate(counts):
             groups.setdefault(n, []).append(i)
@@ -107,6 +107,7 @@ class SafetyFilteringEnvironment:
                 record = out
             else:
                 record[torch.as_tensor(idx, device=dev)] = out
+        risk_metrics.commit_singletons(final)  # only once every launch was accepted
         return HalfspaceBatch(record, setup_time=t1 - t0)
 
     def _pinned_stage(self, n_doubles):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DRCVAR_ABI_VERSION 1
+#define DRCVAR_ABI_VERSION 2 /* 2: MPC options / cluster statuses, per-unit status outputs */
 
 /* return codes */
 #define DRCVAR_OK 0
@@ -67,6 +67,16 @@ extern "C" {
 #define DRCVAR_COL_G_DR_STAR 6  /* g_star of dr_cvar_halfspace() (risk_metrics.py:267) */
 #define DRCVAR_COL_G_DR_TILDE 7 /* DRCVaRSafeHalfspace.g_tilde = g_star - R_c*|h| (risk_metrics.py:299) */
 #define DRCVAR_OUT_WIDTH 8
+
+/* per-unit status word (optional int32 output of the _v2 entry points), a bit set: which of the
+   reference's solver-failure branches the unit took (core/risk_metrics.py:173-177, 261-265,
+   298-303, 334-338), so callers need not infer failure from the sentinel's value */
+#define DRCVAR_UNIT_OK 0
+#define DRCVAR_UNIT_NONFINITE 1    /* a sample is not finite, or the sample sums overflow: every
+                                      offset is the sentinel (both LPs fail) */
+#define DRCVAR_UNIT_UNBOUNDED 2    /* alpha * N > N: both LPs unbounded, every offset the sentinel */
+#define DRCVAR_UNIT_DR_UNBOUNDED 4 /* epsilon < 0: the DR-CVaR LP unbounded (g_star = 100,
+                                      g_dr_tilde = 100 - R_c|h|); the CVaR offset stands */
 
 int drcvar_abi_version(void);
 const char* drcvar_strerror(int code);
@@ -103,6 +113,19 @@ int drcvar_safe_halfspaces_f64_ex(const double* samples, int64_t n_obstacles, in
                                   int32_t threads_per_unit, int32_t samples_per_thread);
 
 /*
+ * drcvar_safe_halfspaces_f64_ex that also writes the per-unit status word (DRCVAR_UNIT_*) into
+ * status[n_obstacles * n_steps] (int32, device; NULL = not written).  Same cost: one 4-B store
+ * per unit.
+ */
+int drcvar_safe_halfspaces_f64_v2(const double* samples, int64_t n_obstacles, int64_t n_steps,
+                                  int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
+                                  int64_t stride_sample, const double* ego_ref_pos,
+                                  int64_t ego_stride_step, double robot_radius,
+                                  double obstacle_radius, double alpha, double delta,
+                                  double epsilon, double* out, int32_t* status, void* stream,
+                                  int32_t threads_per_unit, int32_t samples_per_thread);
+
+/*
  * cvar_halfspace / dr_cvar_halfspace for n_units units with a caller-supplied direction
  * h[u] = (h[u*h_stride_unit], h[u*h_stride_unit + 1]) (not necessarily unit length; the combined
  * radius is scaled by |h| exactly as risk_metrics.py:293 / :234 do).  The output record has the
@@ -113,6 +136,12 @@ int drcvar_offsets_given_h_f64(const double* samples, int64_t n_units, int64_t n
                                int64_t h_stride_unit, double robot_radius, double obstacle_radius,
                                double alpha, double delta, double epsilon, double* out,
                                void* stream);
+/* the same with the per-unit status word (status[n_units], NULL = not written) */
+int drcvar_offsets_given_h_f64_v2(const double* samples, int64_t n_units, int64_t n_samples,
+                                  int64_t stride_unit, int64_t stride_sample, const double* h,
+                                  int64_t h_stride_unit, double robot_radius,
+                                  double obstacle_radius, double alpha, double delta,
+                                  double epsilon, double* out, int32_t* status, void* stream);
 
 /*
  * Host-only query (no device access): the launch geometry chosen for n_samples — threads per

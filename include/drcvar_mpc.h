@@ -60,6 +60,37 @@ extern "C" {
 #define DRCVAR_MPC_STATUS_NUMERICAL 2 /* non-positive pivot or non-finite iterate */
 #define DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE 3 /* stalled with merit <= 1e3*tol; best iterate
                                                   returned (accepted, like mpc_filter.py:154) */
+/* clustered launches only (drcvar_mpc_launch_groups > 1); both roll the fallback inputs out */
+#define DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT 4  /* a workgroup of the problem's cluster did not reach an
+                                                exchange within the spin limit (e.g. it could not be
+                                                made resident beside other work on the device) */
+#define DRCVAR_MPC_STATUS_CLUSTER_DIVERGED 5 /* the cluster's workgroups disagreed on a replicated
+                                                decision (their published state digests differ) */
+
+/*
+ * Per-call options (NULL = every field 0 = the defaults).  No environment variable is read by the
+ * library: what is not set here is the default, and a hipGraph capture freezes what was passed.
+ *   cluster_size      0 = automatic; 1 = one workgroup per problem; c > 1 = clusters of c
+ *                     workgroups where the batch is eligible (capped like the automatic size)
+ *   spin_limit_us     0 = 10000: a cluster exchange that waits longer ends the problem with
+ *                     DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT (fallback rollout) instead of hanging
+ *   debug_*           test hooks (tests/test_mpc_cluster.py), 0 = off:
+ *     debug_force_resume        the first polish gives up at once (exercises the resume round)
+ *     debug_perturb_group       g + 1: workgroup g of every cluster scales its step length by
+ *                               (1 - 2^-20) at interior-point iteration debug_perturb_iteration
+ *                               (must end with DRCVAR_MPC_STATUS_CLUSTER_DIVERGED)
+ *     debug_stall_group         g + 1: workgroup g of every cluster leaves before the final
+ *                               exchange (must end with DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT)
+ */
+typedef struct drcvar_mpc_options {
+  int32_t cluster_size;
+  int32_t spin_limit_us;
+  int32_t debug_force_resume;
+  int32_t debug_perturb_group;
+  int32_t debug_perturb_iteration;
+  int32_t debug_stall_group;
+  int32_t reserved[2];
+} drcvar_mpc_options;
 
 /* Host-side description of a condensed model (filled by drcvar_mpc_model_init). */
 typedef struct drcvar_mpc_model {
@@ -95,12 +126,14 @@ int64_t drcvar_mpc_workspace_doubles(const drcvar_mpc_model* model, int64_t n_pr
  * Workgroups per problem the next drcvar_mpc_filter_f64 launch of this batch shape uses on the
  * current device: 1 (one workgroup per problem), or a cluster of c > 1 workgroups that split the
  * problem's halfspace rows (batches of at most 8 problems with >= 64 obstacles: one workgroup per
- * 16 obstacles, c <= 32 and c * n_problems <= the device's CUs; the environment variable
- * DRCVAR_MPC_CLUSTER=<c> sets c within those limits, 1 selects the one-workgroup form).
+ * 16 obstacles, c <= 32 and c * n_problems <= half the device's CUs, so that a clustered launch
+ * stays resident beside other work).  The _ex form applies options->cluster_size.
  * Host query (reads the device's CU count).  -1 on invalid arguments.
  */
 int32_t drcvar_mpc_launch_groups(const drcvar_mpc_model* model, int64_t n_problems,
                                  int64_t n_obstacles);
+int32_t drcvar_mpc_launch_groups_ex(const drcvar_mpc_model* model, int64_t n_problems,
+                                    int64_t n_obstacles, const drcvar_mpc_options* options);
 
 /*
  * Solve n_problems independent safety-filter QPs.
@@ -137,6 +170,17 @@ int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int
                           double tol, int32_t polish, double* x_out, double* u_out,
                           double* info_out, double* workspace, int64_t workspace_doubles,
                           void* stream);
+/* drcvar_mpc_filter_f64 with per-call options (NULL = defaults; see drcvar_mpc_options) */
+int drcvar_mpc_filter_f64_ex(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
+                             const double* hs_h, const double* hs_g, int64_t n_obstacles,
+                             int64_t n_hs_steps, int64_t h_sp, int64_t h_so, int64_t h_sk,
+                             int64_t g_sp, int64_t g_so, int64_t g_sk, const double* x0,
+                             int64_t x0_sp, const double* x_ref, int64_t xr_sp, int64_t xr_st,
+                             const double* u_fallback, int64_t uf_sp, int64_t uf_st,
+                             int32_t max_iter, double tol, int32_t polish, double* x_out,
+                             double* u_out, double* info_out, double* workspace,
+                             int64_t workspace_doubles, const drcvar_mpc_options* options,
+                             void* stream);
 
 #ifdef __cplusplus
 }

@@ -48,25 +48,28 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=["30,3,1", "30,3,3", "30,3,1024", "20,10,3",
                                                     "50,256,1", "50,256,3"])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--cluster", type=int, default=0,
+                    help="workgroups per problem (drcvar_mpc_options.cluster_size; 0 = automatic, 1 = one)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    opt = mf.make_options(cluster_size=args.cluster)
     for shape in args.shapes:
         H, O, B = (int(v) for v in shape.split(","))
         model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
         h, g = rec[..., 3:5], rec[..., 7]
         ws = torch.empty(model.workspace_doubles(B, O), dtype=torch.float64, device=dev)
-        x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws)
+        x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt)
         torch.cuda.synchronize()
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record()
         for _ in range(args.reps):
-            x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws)
+            x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt)
         t1.record()
         torch.cuda.synchronize()
         ms = t0.elapsed_time(t1) / args.reps
         inf = info.cpu().numpy()
         st = inf[:, _native.MPC_INFO_STATUS]
-        print(f"H={H} O={O} B={B} groups={model.launch_groups(B, O)}: {ms:.3f} ms/launch, "
+        print(f"H={H} O={O} B={B} groups={model.launch_groups(B, O, opt)}: {ms:.3f} ms/launch, "
               f"{B / ms * 1e3:.0f} QPs/s, "
               f"iters {inf[:, _native.MPC_INFO_ITERATIONS].mean():.1f}, "
               f"polished {inf[:, _native.MPC_INFO_POLISHED].mean():.2f}, "

@@ -43,7 +43,7 @@ def test_library_holds_gfx950_code_object():
 
 def test_abi_version_and_strerror():
     lib = _native.lib()
-    assert lib.drcvar_abi_version() == _native.ABI_VERSION == 1
+    assert lib.drcvar_abi_version() == _native.ABI_VERSION == 2
     assert lib.drcvar_strerror(0) == b"ok"
     assert lib.drcvar_strerror(1) == b"invalid argument"
     assert lib.drcvar_strerror(99) == b"unknown error"

@@ -2,11 +2,15 @@
 (core/mpc_filter.py:116-151 with many obstacles, e.g. the C5 hand-off's 12 800 halfspace rows) on
 several workgroups that split the rows and exchange their row sums inside the launch.
 
-CPU: the workspace layout of clustered shapes.  GPU: clustered launches against the oracle
-(oracle/mpc_qp.py, KKT-certified) and against the one-workgroup form (DRCVAR_MPC_CLUSTER=1) —
-C5 hand-off shape, uneven obstacle slices, several problems per launch, every cluster size cap,
-run-to-run bitwise determinism and hipGraph capture/replay (a one-wave kernel re-zeroes the
-counters in front of every replay).  Tolerance as tests/test_mpc.py: MPC_TOL on inputs and states.
+CPU: the workspace layout of clustered shapes, the options struct.  GPU: clustered launches
+against the oracle (oracle/mpc_qp.py, KKT-certified) and against the one-workgroup form
+(options.cluster_size = 1) — C5 hand-off shape, uneven obstacle slices, several problems per
+launch, every cluster size cap, run-to-run bitwise determinism and hipGraph capture/replay (a
+one-wave kernel re-zeroes the counters in front of every replay); the cluster's failure modes
+through the debug hooks: a workgroup whose replicated decision drifts (CLUSTER_DIVERGED, ended at
+the next exchange) and a workgroup that never reaches the final exchange (CLUSTER_TIMEOUT, the
+fallback rollout returned even though the solve itself had converged).  Tolerance as
+tests/test_mpc.py: MPC_TOL on inputs and states.
 """
 import ctypes
 import os
@@ -32,14 +36,22 @@ def test_cluster_workspace_layout(B, O, groups):
         assert ws == B * (CTRL + ROWS * O + min(O, 32, 256 // B) * (BEST + 2 * REC))
 
 
+def test_options_struct_layout():
+    """drcvar_mpc_options: eight int32 fields (include/drcvar_mpc.h), 0-based hook groups in the
+    Python helper become the header's g + 1 encoding."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    assert ctypes.sizeof(_native.MpcOptions) == 32
+    o = mf.make_options(cluster_size=3, debug_perturb_group=0, debug_perturb_iteration=2)
+    assert (o.cluster_size, o.debug_perturb_group, o.debug_perturb_iteration, o.debug_stall_group) == (3, 1, 2, 0)
+    assert mf.STATUS_NAMES[_native.MPC_STATUS_CLUSTER_TIMEOUT] == "cluster_timeout"
+    assert mf.STATUS_NAMES[_native.MPC_STATUS_CLUSTER_DIVERGED] == "cluster_diverged"
+
+
 @pytest.fixture()
-def cluster_size(monkeypatch):
-    def set_size(c):
-        if c is None:
-            monkeypatch.delenv("DRCVAR_MPC_CLUSTER", raising=False)
-        else:
-            monkeypatch.setenv("DRCVAR_MPC_CLUSTER", str(c))
-    return set_size
+def cluster_size():
+    """Options selecting the cluster size (None = automatic, 1 = one workgroup per problem)."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    return lambda c: mf.make_options(cluster_size=0 if c is None else c)
 
 
 @pytest.fixture(scope="module")
@@ -68,7 +80,7 @@ def _batch(dyn, H, O, B, tight, seed):
     return probs
 
 
-def _solve(probs, dev):
+def _solve(probs, dev, options=None, timed=False):
     import torch
     from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
     p0 = probs[0]
@@ -76,11 +88,23 @@ def _solve(probs, dev):
                         device=dev)
     T_ = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
     hs = T_(np.stack([p["hs"] for p in probs]))
-    x, u, info = mf.filter_batch(model, hs[..., 0:2], hs[..., 2], T_(np.stack([p["x0"] for p in probs])),
-                                 T_(np.stack([p["x_ref"] for p in probs])),
-                                 T_(np.stack([p["u_ref"] for p in probs])))
-    groups = model.launch_groups(len(probs), hs.shape[1])
-    return x.cpu().numpy(), u.cpu().numpy(), info.cpu().numpy(), groups
+    args = (model, hs[..., 0:2], hs[..., 2], T_(np.stack([p["x0"] for p in probs])),
+            T_(np.stack([p["x_ref"] for p in probs])), T_(np.stack([p["u_ref"] for p in probs])))
+    ws = torch.empty(model.workspace_doubles(len(probs), hs.shape[1]), dtype=torch.float64, device=dev)
+    if timed:  # the launch's own duration (HIP events on the launching stream), after a warm-up
+        mf.filter_batch(*args, workspace=ws, options=options)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    x, u, info = mf.filter_batch(*args, workspace=ws, options=options)
+    ms = None
+    if timed:
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+    groups = model.launch_groups(len(probs), hs.shape[1], options)
+    out = (x.cpu().numpy(), u.cpu().numpy(), info.cpu().numpy(), groups)
+    return out + (ms,) if timed else out
 
 
 def _check_vs_oracle(probs, x, u, info, label):
@@ -109,16 +133,14 @@ def _check_vs_oracle(probs, x, u, info, label):
 ])
 def test_gpu_cluster_matches_oracle_and_one_workgroup(dyn, H, O, B, tight, dev, cluster_size):
     probs = _batch(dyn, H, O, B, tight, seed=H * 1000 + O + B)
-    cluster_size(None)
-    x, u, info, groups = _solve(probs, dev)
+    x, u, info, groups = _solve(probs, dev, cluster_size(None))
     assert groups > 1
     _check_vs_oracle(probs, x, u, info, f"cluster x{groups}")
-    x2, u2, info2, _ = _solve(probs, dev)  # run to run: the same bits
+    x2, u2, info2, _ = _solve(probs, dev, cluster_size(None))  # run to run: the same bits
     np.testing.assert_array_equal(u, u2)
     np.testing.assert_array_equal(x, x2)
     np.testing.assert_array_equal(info, info2)
-    cluster_size(1)
-    x1, u1, info1, g1 = _solve(probs, dev)
+    x1, u1, info1, g1 = _solve(probs, dev, cluster_size(1))
     assert g1 == 1
     _check_vs_oracle(probs, x1, u1, info1, "one workgroup")
 
@@ -126,11 +148,10 @@ def test_gpu_cluster_matches_oracle_and_one_workgroup(dyn, H, O, B, tight, dev, 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cap", [2, 3, 5, 16, 31])
 def test_gpu_cluster_every_size(cap, dev, cluster_size):
-    """The same C5-shaped problem on clusters of 2..31 workgroups (DRCVAR_MPC_CLUSTER; slices of
-    8 to 128 obstacles, even and uneven)."""
+    """The same C5-shaped problem on clusters of 2..31 workgroups (options.cluster_size; slices
+    of 8 to 128 obstacles, even and uneven)."""
     probs = _batch("double", 50, 256, 1, False, seed=5)
-    cluster_size(cap)
-    x, u, info, groups = _solve(probs, dev)
+    x, u, info, groups = _solve(probs, dev, cluster_size(cap))
     assert groups == cap
     _check_vs_oracle(probs, x, u, info, f"cluster x{cap}")
 
@@ -142,7 +163,6 @@ def test_gpu_cluster_graph_replay(dev, cluster_size):
     of the counters failed from the second replay on)."""
     import torch
     from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
-    cluster_size(None)
     probs = _batch("double", 50, 256, 2, False, seed=9)
     p0 = probs[0]
     model = mf.MPCModel(p0["A"], p0["B"], p0["C"], p0["Q"], p0["R"], p0["H"], p0["ub"], p0["pb"],
@@ -175,19 +195,78 @@ def test_gpu_cluster_graph_replay(dev, cluster_size):
     ("double", 30, 6, 3, True),     # one workgroup per problem
     ("generic3", 24, 70, 2, True),  # clustered, three inputs
 ])
-def test_gpu_resume_after_failed_polish(dyn, H, O, B, tight, dev, cluster_size, monkeypatch):
-    """DRCVAR_MPC_FORCE_RESUME=1 makes the first polish give up at once, so every problem takes
+def test_gpu_resume_after_failed_polish(dyn, H, O, B, tight, dev):
+    """options.debug_force_resume makes the first polish give up at once, so every problem takes
     the resume round (csrc/drcvar_mpc.hip, ipm_round): the interior-point state the polish
     overwrote is restored (the rows' s / w_hs, the bound states, u), the method continues towards
     tol * 1e-3 and polishes again.  The answer must match the oracle and the normal path."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
     probs = _batch(dyn, H, O, B, tight, seed=7 * H + O + B)
-    cluster_size(None)
     x, u, info, _ = _solve(probs, dev)
-    monkeypatch.setenv("DRCVAR_MPC_FORCE_RESUME", "1")
-    x2, u2, info2, _ = _solve(probs, dev)
+    x2, u2, info2, _ = _solve(probs, dev, mf.make_options(debug_force_resume=True))
     _check_vs_oracle(probs, x2, u2, info2, "resumed")
     assert np.all(info2[:, _native.MPC_INFO_ITERATIONS] >= info[:, _native.MPC_INFO_ITERATIONS])
     assert np.all(info2[:, _native.MPC_INFO_POLISH_ATTEMPTS] >= 1)
     both = (info[:, _native.MPC_INFO_POLISHED] == 1) & (info2[:, _native.MPC_INFO_POLISHED] == 1)
     np.testing.assert_allclose(u2[both], u[both], atol=MPC_TOL)
     np.testing.assert_allclose(x2[both], x[both], atol=MPC_TOL)
+
+
+def _fallback_rollout(pr):
+    """x, u of the fallback inputs rolled out from x0 (core/mpc_filter.py:211-217)."""
+    u = np.asarray(pr["u_ref"], dtype=np.float64)
+    x = np.zeros((pr["H"] + 1, pr["A"].shape[0]))
+    x[0] = pr["x0"]
+    for t in range(pr["H"]):
+        x[t + 1] = pr["A"] @ x[t] + pr["B"] @ u[t]
+    return x, u
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group,iteration", [(3, 2), (0, 5), (15, 1)])
+def test_gpu_cluster_divergence_is_detected(group, iteration, dev):
+    """One workgroup of the C5-shaped cluster scales its step length by (1 - 2^-20) at one
+    interior-point iteration (options.debug_perturb_*): its state digest no longer matches the
+    others' at the next exchange, so every workgroup ends the problem there — status
+    CLUSTER_DIVERGED, the fallback inputs rolled out — in well under a millisecond, instead of
+    combining records of different sites or spinning to the time limit."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    probs = _batch("double", 50, 256, 1, False, seed=11)
+    x, u, info, groups, ms = _solve(probs, dev, mf.make_options(debug_perturb_group=group,
+                                                                debug_perturb_iteration=iteration),
+                                    timed=True)
+    assert groups == 16
+    assert int(info[0, _native.MPC_INFO_STATUS]) == _native.MPC_STATUS_CLUSTER_DIVERGED, info[0]
+    assert info[0, _native.MPC_INFO_USED_FALLBACK] == 1
+    assert np.isnan(info[0, _native.MPC_INFO_OBJECTIVE])
+    assert int(info[0, _native.MPC_INFO_ITERATIONS]) <= iteration + 1
+    xf, uf = _fallback_rollout(probs[0])
+    np.testing.assert_array_equal(u[0], uf)
+    np.testing.assert_allclose(x[0], xf, atol=1e-12)
+    assert ms < 1.0, f"divergence took {ms:.3f} ms to end the launch"
+    # the same problem unperturbed converges (the hook is the only difference)
+    _, _, info0, _ = _solve(probs, dev)
+    assert int(info0[0, _native.MPC_INFO_STATUS]) == _native.MPC_STATUS_OPTIMAL
+
+
+@pytest.mark.gpu
+def test_gpu_cluster_timeout_at_final_exchange_rolls_out_fallback(dev):
+    """Workgroup 5 of the cluster leaves before the final exchange (options.debug_stall_group):
+    every other workgroup's wait there gives up after spin_limit_us, and although the
+    interior-point solve had converged, the problem must report CLUSTER_TIMEOUT with the fallback
+    inputs rolled out and no objective — outputs consistent with the status (the reference's
+    fallback semantics, core/mpc_filter.py:166-178)."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    probs = _batch("double", 50, 256, 1, False, seed=13)
+    x, u, info, groups, ms = _solve(probs, dev, mf.make_options(debug_stall_group=5, spin_limit_us=300),
+                                    timed=True)
+    assert groups == 16
+    assert int(info[0, _native.MPC_INFO_STATUS]) == _native.MPC_STATUS_CLUSTER_TIMEOUT, info[0]
+    assert info[0, _native.MPC_INFO_USED_FALLBACK] == 1
+    assert np.isnan(info[0, _native.MPC_INFO_OBJECTIVE]) and np.isnan(info[0, _native.MPC_INFO_MAX_SLACK])
+    xf, uf = _fallback_rollout(probs[0])
+    np.testing.assert_array_equal(u[0], uf)
+    np.testing.assert_allclose(x[0], xf, atol=1e-12)
+    assert ms < 5.0, f"timeout path took {ms:.3f} ms"
+    # the surface wrapper reports it as a failed solve with the fallback (core/mpc_filter.py:168-173)
+    assert mf.STATUS_NAMES[int(info[0, _native.MPC_INFO_STATUS])] not in mf.SOLVED

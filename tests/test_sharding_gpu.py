@@ -126,3 +126,28 @@ def test_rccl_world1_sharded_batch_step_eager_and_graph(dev, rccl_group):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(sb.records(), want)
+
+
+def test_rccl_world1_c4_leg_phases(dev, rccl_group):
+    """bench.py's C4 strong-scaling leg (BASELINE config 4: 64 obstacles x T 30 x N 5000, the
+    RCCL all-gather config) on a 1-rank RCCL group with the collective forced on: the stepper of
+    the whole step, of the kernel alone and of the all-gather alone (the phase splits the leg
+    reports), graph-captured; the gathered records equal the single-launch evaluation of the
+    same batch, and the C oracle on a strided subset of units."""
+    import bench
+    O, T, N = bench.WORKLOADS["c4"][:3]
+    nominal, ego = _nominal(O, T, dev, seed=11)
+    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, group=rccl_group, seed=11)
+    sb.full = torch.full((sb.per, 8), float("nan"), dtype=torch.float64, device=dev)  # force the collective
+    whole_s, _ = synthetic.obstacle_batch(O, T, N, dev, seed=11)
+    want = engine.safe_halfspaces(whole_s, ego, RiskParams())
+    for kw in ({}, {"exchange": False}, {"compute": False}):
+        st = bench.Stepper(sb, "graph", 10, 20, dev, warmup=5, **kw)
+        assert st.fallback is None, st.fallback
+        assert st.run(5) == 5 and st.run(20) == 20
+        torch.cuda.synchronize()
+        assert "step = " in st.describe()
+    assert torch.equal(sb.records(), want)
+    sub = slice(0, O, 9)
+    ref = _oracle(whole_s[sub], ego)
+    assert np.max(np.abs(sb.records()[sub].cpu().numpy() - ref)) < OFFSET_TOL
