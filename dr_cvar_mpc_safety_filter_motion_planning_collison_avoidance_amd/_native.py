@@ -126,7 +126,9 @@ def build(verbose: bool = False, extra_flags=()) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     obj_dir = os.path.join(LIB_DIR, "obj")
     os.makedirs(obj_dir, exist_ok=True)
-    headers = b"".join(open(h, "rb").read() for h in HEADERS)
+    import glob
+    incs = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.inc")))  # tables the sources include
+    headers = b"".join(open(h, "rb").read() for h in HEADERS + incs)
     objs, procs = [], []
     for src, defs in _compile_units():
         flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-I", INCLUDE_DIR,

@@ -482,6 +482,10 @@ struct LinearMap {
   __device__ __forceinline__ double operator()(double d) const { return fma(d, scale, off); }
 };
 
+// LDS accesses of one wave complete in order; this keeps the compiler from moving them across a
+// wave-local hand-off (no barrier needed within a wave)
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
 // Per-wave ordered compaction step: append the candidates of one row to this wave's LDS region.
 __device__ __forceinline__ void append_candidate(double* region, uint32_t& wbase, bool is_cand,
                                                  double v, unsigned long long lt_mask) {
@@ -742,8 +746,20 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
                       Params prm, double* __restrict__ out, int32_t* __restrict__ status) {
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << LOG_NB;
+  // window lists (small plans, -DDRCVAR_WINLIST): every in-window sample is kept in its wave's
+  // LDS list during the window pass, so after barrier 2 wave 0 finishes alone (no candidate pass,
+  // no barrier 3).  MEASURED AND NOT KEPT (round 3): C3 4.73 -> 6.05 us per step (HIP events) —
+  // wave 0's serial pass over ~300 window values (a ballot compaction per slot) is longer than
+  // the parallel candidate pass + barrier 3 it replaces.
+#ifdef DRCVAR_WINLIST
+  constexpr bool kList = P <= 8;
+#else
+  constexpr bool kList = false;
+#endif
   __shared__ uint32_t hist[hist_words<NB>()];
   __shared__ double cand[NW * kCap];
+  __shared__ double win[kList ? NW * P * kWave : 1];
+  __shared__ double lane_tail[kList ? BLOCK : 1];
   __shared__ uint32_t wcount[NW];
   __shared__ uint32_t wbelow_sh[NW];
   __shared__ double red_mom[2 * NW];
@@ -889,6 +905,8 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   double sq = 0.0;  // sum over samples below the target bucket of (d - mu_d)
   if (fast) {
     uint32_t wbelow = 0;  // samples of this wave below the window (wave-uniform)
+    uint32_t wlist = 0;   // samples of this wave in the window (list length, wave-uniform)
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const double v = d[j];
@@ -899,9 +917,17 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       const bool inw = !low && tv < kNB;
       const int b = inw ? static_cast<int>(tv) : 0;  // 0 <= b <= NB - 1 inside the window
       if (inw) atomicAdd(&hist[hist_slot<NB>(b)], 1u);
-      const uint32_t cj = inw ? static_cast<uint32_t>(b) : 0xFFFFu;
-      if (j % 2 == 0) code[j / 2] = cj;
-      else code[j / 2] |= cj << 16;
+      if constexpr (kList) {
+        append_candidate(win + wave * (P * kWave), wlist, inw, v, lt_mask);
+      } else {
+        const uint32_t cj = inw ? static_cast<uint32_t>(b) : 0xFFFFu;
+        if (j % 2 == 0) code[j / 2] = cj;
+        else code[j / 2] |= cj << 16;
+      }
+    }
+    if constexpr (kList) {
+      lane_tail[tid] = sq;  // below-window partial sums, combined by wave 0 in a fixed order
+      if (lane == 0) wcount[wave] = wlist;
     }
     if (lane == 0) wbelow_sh[wave] = wbelow;
     DRCVAR_STAMP(3);
@@ -930,7 +956,43 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // ---- 4. candidates of the target bucket + tail sum below them -----------------------------
   double tau, dsum;  // dsum = sum_{d<tau} (d - tau)
   double rch;        // R_c |h| (risk_metrics.py:293, :234), wave 0
-  if (fast) [[likely]] {
+  if (kList && fast) [[likely]] {
+    // wave 0 alone: the target bucket's candidates and the in-window part of the tail sum come
+    // from the waves' window lists (each value re-binned by the same fma as in the window pass,
+    // so the classification is identical); the order of every sum is fixed
+    if (wave != 0) {
+      if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
+      return;
+    }
+    DRCVAR_STAMP(5);
+    const uint32_t ubin = static_cast<uint32_t>(bin);
+    double tail = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tail += lane_tail[w * kWave + lane];
+    uint32_t ccount = 0;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t nw = wcount[w];
+#pragma unroll
+      for (int r = 0; r < P; ++r) {
+        const uint32_t idx = static_cast<uint32_t>(r * kWave + lane);
+        const bool in = idx < nw;
+        const double v = in ? win[w * (P * kWave) + idx] : 0.0;
+        const uint32_t b = static_cast<uint32_t>(map(v));  // in-window values: 0 <= b < NB
+        tail += (in && b < ubin) ? v - mu_d : 0.0;
+        append_candidate(cand, ccount, in && b == ubin, v, lt_mask);
+      }
+    }
+    const double s_below = wave_reduce<OpAdd>(tail);
+    rch = prm.rc * norm_h(h0, h1);  // R_c |h|
+    if (lane == 0) wcount[0] = ccount;  // the candidates as one region (wave-local hand-off)
+    wave_lds_fence();
+    double s_cand;
+    tau = rank_candidates<1>(cand, wcount, c, rr, lane, &s_cand);
+    dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
+    DRCVAR_STAMP(6);
+  } else if (fast) [[likely]] {
     uint32_t wbase = 0;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const uint32_t ubin = static_cast<uint32_t>(bin);

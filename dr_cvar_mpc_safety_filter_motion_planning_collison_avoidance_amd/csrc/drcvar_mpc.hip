@@ -609,6 +609,147 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[N
   return ok;
 }
 
+// Factorisation for NX = 4 (the reference's double integrator and every smaller model) with the
+// recursion's state in registers: lane (i, j) of a 16-lane row holds P_{k+1}[i][j], and a step
+// moves data between lanes only through the cross-lane paths of the register file — DPP quad
+// broadcasts for a row of a matrix (lane (i, m) -> every lane of quad i) and ds_swizzle bit-mask
+// patterns for a column (lane (m, j) -> every lane of column j: the LDS crossbar, no LDS memory,
+// no fence) — instead of the two LDS hand-offs per step of the entry-by-entry form below:
+//   T = P A (lane (i, j)), U = P B (row i, every lane of it); columns of T and all of U by swizzle
+//   Re = Rb + B'U, its inverse (every lane, identical operands in canonical order: uniform)
+//   L[:, i] = U'A[:, i], L[:, j] = U'A[:, j] (the same formula for both columns, so mirrored lanes
+//   see the same values), Kg[:, j] = Re^-1 L[:, j]
+//   P_k = Qb_k + (A'T)[i][j] - L[:, i]' Re^-1 L[:, j]
+// Qb and L'Re^-1 L are evaluated in a form whose rounding is symmetric in (i, j) (no fma
+// contraction, commutative products and pair sums); A'PA is not, so P_k is mirrored from its
+// lower triangle by one ds_bpermute (the recursion must stay exactly symmetric, see above).
+// Every row of wave 0 computes the same (rows 1..3 replicate row 0; only row 0 stores).
+// MEASURED AND NOT KEPT (round 3; build with -DDRCVAR_MPC_RICCATI_REGS): C5 QP 0.948 -> 1.033 ms,
+// main.py's 1024-problem batch 0.559 -> 0.751 ms, and the generic3 H = 40 test 8.5e-6 off the
+// oracle.  ds_swizzle and ds_bpermute go through the LDS unit like the reads they replace (two
+// hand-offs per step either way), there are 26 of them per step, and computing L from U = PB
+// instead of from T = PA decorrelates the rounding of the two huge terms whose difference is P.
+template <int M>
+__device__ __forceinline__ double qrow_f64(double v) {  // lane (i, M) of quad i, to the quad
+  constexpr int ctrl = M | (M << 2) | (M << 4) | (M << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int M>
+__device__ __forceinline__ double qcol_f64(double v) {  // lane (M, j) of the row of 16, to lane (*, j)
+  constexpr int pattern = 0x3 | ((M << 2) << 5);      // bit-mask mode: (lane & 3) | (M << 2)
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pattern);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pattern);
+  return __hiloint2double(hi, lo);
+}
+
+template <int NU>
+__device__ inline bool riccati_factor_regs4(const Lds& s, int H) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int e = lane & 15, i = e >> 2, j = e & 3;
+  const int tr_addr = 4 * ((lane & ~15) | (j * 4 + i));  // the transposed entry's lane
+  double Aj[4], Ai[4], Bm[4][NU], R2[NU][NU];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    Aj[m] = s.Am[m * kMx + j];
+    Ai[m] = s.Am[m * kMx + i];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) Bm[m][c] = s.Bm[m * NU + c];
+  }
+#pragma unroll
+  for (int c = 0; c < NU; ++c)
+#pragma unroll
+    for (int d = 0; d < NU; ++d) R2[c][d] = 2.0 * s.Rm[c * NU + d];
+  const double c0i = s.Cm[i], c1i = s.Cm[kMx + i], c0j = s.Cm[j], c1j = s.Cm[kMx + j];
+  const double q2 = s.Qm[i * kMx + j] + s.Qm[j * kMx + i];  // 2Q for a symmetric Q, symmetric always
+  const double cc00 = c0i * c0j, cc11 = c1i * c1j, cc01 = c0i * c1j + c1i * c0j;
+  auto qb = [&](int k) {  // Qb_{k+1} = 2Q + C'S_k C, entry (i, j), symmetric rounding
+    const double S00 = s.S[k], S01 = s.S[H + k], S11 = s.S[2 * H + k];
+    return q2 + ((S00 * cc00 + S11 * cc11) + S01 * cc01);
+  };
+  double p = qb(H - 1);
+  bool ok = true;
+  for (int k = H - 1; k >= 0 && ok; --k) {
+    double du[NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) du[c] = s.DU[k * NU + c];
+    const double qnext = k > 0 ? qb(k - 1) : 0.0;
+    // row i of P
+    const double r0 = qrow_f64<0>(p), r1 = qrow_f64<1>(p), r2 = qrow_f64<2>(p), r3 = qrow_f64<3>(p);
+    // T[i][j] = P[i,:] A[:, j], U[i][c] = P[i,:] B[:, c]
+    const double t = (r0 * Aj[0] + r1 * Aj[1]) + (r2 * Aj[2] + r3 * Aj[3]);
+    double u[NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) u[c] = (r0 * Bm[0][c] + r1 * Bm[1][c]) + (r2 * Bm[2][c] + r3 * Bm[3][c]);
+    // column j of T, all of U (canonical row order m = 0..3)
+    const double tc[4] = {qcol_f64<0>(t), qcol_f64<1>(t), qcol_f64<2>(t), qcol_f64<3>(t)};
+    double uc[4][NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+      uc[0][c] = qcol_f64<0>(u[c]);
+      uc[1][c] = qcol_f64<1>(u[c]);
+      uc[2][c] = qcol_f64<2>(u[c]);
+      uc[3][c] = qcol_f64<3>(u[c]);
+    }
+    // Re = Rb + B'U (upper triangle, mirrored: exactly symmetric) and its inverse
+    double Re[NU][NU], Ri[NU][NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c)
+#pragma unroll
+      for (int d = c; d < NU; ++d) {
+        const double bu = (Bm[0][c] * uc[0][d] + Bm[1][c] * uc[1][d]) + (Bm[2][c] * uc[2][d] + Bm[3][c] * uc[3][d]);
+        Re[c][d] = (R2[c][d] + (c == d ? du[c] : 0.0)) + bu;
+        Re[d][c] = Re[c][d];
+      }
+    ok = spd_inverse<NU>(Re, Ri);
+#pragma unroll
+    for (int c = 0; c < NU; ++c)
+#pragma unroll
+      for (int d = c + 1; d < NU; ++d) Ri[d][c] = Ri[c][d];
+    // L[:, i] and L[:, j] by one formula, L[c][x] = sum_n U[n][c] A[n][x]
+    double Li[NU], Lj[NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+      Li[c] = (uc[0][c] * Ai[0] + uc[1][c] * Ai[1]) + (uc[2][c] * Ai[2] + uc[3][c] * Ai[3]);
+      Lj[c] = (uc[0][c] * Aj[0] + uc[1][c] * Aj[1]) + (uc[2][c] * Aj[2] + uc[3][c] * Aj[3]);
+    }
+    // L[:, i]' Re^-1 L[:, j] with (i, j)-symmetric rounding: diagonal terms Ri_cc (Li_c Lj_c),
+    // pairs Ri_cd (Li_c Lj_d + Li_d Lj_c)
+    double corr = 0.0;
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+      corr = corr + Ri[c][c] * (Li[c] * Lj[c]);
+#pragma unroll
+      for (int d = c + 1; d < NU; ++d) corr = corr + Ri[c][d] * (Li[c] * Lj[d] + Li[d] * Lj[c]);
+    }
+    const double apa = (Ai[0] * tc[0] + Ai[1] * tc[1]) + (Ai[2] * tc[2] + Ai[3] * tc[3]);
+    const double pn = (qnext + apa) - corr;
+    // mirror the lower triangle
+    const int plo = __builtin_amdgcn_ds_bpermute(tr_addr, __double2loint(pn));
+    const int phi = __builtin_amdgcn_ds_bpermute(tr_addr, __double2hiint(pn));
+    p = i >= j ? pn : __hiloint2double(phi, plo);
+    // gains Kg[:, j] = Re^-1 L[:, j] (row 0 of the wave stores column j), Re^-1 (lane 0)
+    if (lane < 4) {
+#pragma unroll
+      for (int c = 0; c < NU; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int d = 0; d < NU; ++d) acc = acc + Ri[c][d] * Lj[d];
+        s.Kg[(k * NU + c) * 4 + j] = acc;
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < NU; ++c)
+#pragma unroll
+        for (int d = 0; d < NU; ++d) s.Ri[(k * NU + c) * NU + d] = Ri[c][d];
+    }
+  }
+  return ok;
+}
+
 // Factorisation: Kg_k and Re_k^-1 for every step into LDS (s.Kg, s.Ri).  Uses s.S (per-step 2x2
 // position weights) and s.DU (input weights).  NX = the state dimension padded to 4 or 8: the
 // model matrices are zero-padded in LDS (setup), so every padded entry of P, T, U, Kg is exactly
@@ -618,6 +759,14 @@ template <int NU, int NX, bool kStationary = false>
 __device__ inline bool riccati_factor(const Lds& s, int H) {
   const int tid = threadIdx.x, lane = tid & 63;
   double* flag = s.sc + 62;
+#ifdef DRCVAR_MPC_RICCATI_REGS  // measured slower, kept for the record
+  if constexpr (NX == 4 && !kStationary) {  // the register form (above)
+    if (tid < 64) {
+      const bool ok = riccati_factor_regs4<NU>(s, H);
+      if (lane == 0) *flag = ok ? 0.0 : 1.0;
+    }
+  } else
+#endif
   if (tid < 64) {
     constexpr int NX2 = NX * NX;
     const int e = lane < NX2 ? lane : 0;

@@ -2,25 +2,29 @@
 //
 // Reference: simulation/obstacles.py:43-77 (generate_obstacle_sample_trajectories): for every step
 // t >= 1 the N samples are nominal[t] + N(0, noise_cov) (np.random.multivariate_normal), step 0 is
-// the nominal start for every sample (:63).  Here every sample is one Philox4x32-10 call (counter =
-// global sample index and stream, key = seed) -> two 53-bit uniforms -> Box-Muller -> L z, written
-// straight into the [O, T, N, 2] layout the halfspace kernel streams.
+// the nominal start for every sample (:63).  Here every PAIR of samples (2p, 2p + 1) of a unit is
+// one Philox4x32-10 call (counter = (unit * ceil(N/2) + p, stream), key = seed): its four 32-bit
+// words are two (radius, angle) uniform pairs -> Box-Muller -> L z, written straight into the
+// [O, T, N, 2] layout the halfspace kernel streams.
 //
-// The per-sample arithmetic is what bounds this kernel, not the 16-B store: with the library's
-// fp64 log (98 VALU instructions) and sincospi (71) plus Philox's 40 quarter-rate 32-bit
-// multiplies it ran at 0.21 of HBM.  So the Box-Muller pieces are written for this input domain:
-//   * Philox rounds use one v_mad_u64_u32 per product (the 64-bit product gives both halves) and
-//     one v_bitop3_b32 (3-input XOR, truth table 0x96) per output word;
-//   * log u1 for u1 in (0, 1): frexp, f = m - 1 with m in [sqrt(1/2), sqrt(2)), s = f / (2 + f),
-//     log(1 + f) = 2 atanh(s) as a degree-21 odd series in s (|s| <= 0.1716: truncation < 1e-17);
-//   * cos/sin of 2 pi u2 straight from the 64 raw bits of u2: the top two bits (rounded) are the
-//     quadrant, the signed remainder |x| <= pi/4 goes through Taylor series to x^15 / x^16;
+// The per-sample arithmetic bounds this kernel, not the 16-B store (round 2: 163 VALU instructions
+// per sample, 0.33 of HBM, VALU busy 1.02).  This form (round 3):
+//   * one Philox call per two samples (32-bit uniforms: radius up to 6.8 sd, angle resolution
+//     2^-32 turn) — half the 20 v_mad_u64_u32 + 20 v_bitop3_b32 per sample;
+//   * log u for u = (x + 1/2) 2^-32: frexp, the mantissa's top 7 bits (rounded) pick the nearest
+//     of 65 centres c_k (1/c_k and -log(1/c_k) in constant memory), r = m / c_k - 1 by one fma
+//     (|r| <= 1/128),
+//     log1p(r) to r^8 (truncation < 2e-20) — instead of a rcp/Newton division and a degree-21
+//     series;
+//   * cos / sin of 2 pi w / 2^32: the top 7 bits (rounded) pick the nearest of 128 table angles,
+//     the signed remainder |b| <= pi/128 goes through sin b to b^7 and cos b - 1 to b^6, rotated by
+//     the table point — instead of a quadrant fold and series to x^15 / x^16;
 //   * sqrt through rsq + Newton (the argument is never denormal);
-//   * the series' Horner steps as v_fma_f64 with the coefficient in SGPRs (fma_sc): the compiler
-//     otherwise copied a VGPR-held coefficient into the accumulator before each v_fmac_f64
-//     (190 -> 163 VALU instructions per sample, 0.838 -> 0.775 ms per 128 M samples, same bits);
-// All four agree with the libm functions to a few ulp (tests/test_sampling.py checks the host
-// mirror oracle/philox_sampler.py against numpy's log/sin/cos and the kernel against the mirror).
+//   * the series' Horner steps as v_fma_f64 with the coefficient in SGPRs (fma_sc).
+// The tables are generated once (scripts/gen_sampler_tables.py, extended precision, exact hex
+// literals in drcvar_sampling_tables.inc); the host mirror oracle/philox_sampler.py reads the same
+// file.  Accuracy: log within a few ulp, cos / sin within ~2e-16 of extended-precision references
+// (tests/test_sampling.py); kernel vs mirror to 1e-14 (FMA contraction only).
 
 #include <hip/hip_runtime.h>
 
@@ -31,7 +35,9 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kPerThread = 4;  // samples per thread (independent Philox calls for ILP)
+constexpr int kPairs = 2;  // sample pairs per thread (independent Philox calls for ILP)
+
+#include "drcvar_sampling_tables.inc"
 
 struct Philox {
   uint32_t x[4];
@@ -66,50 +72,40 @@ __device__ __forceinline__ double fma_sc(double a, double b, double c) {
   return r;
 }
 
-// Uniform in the open interval (0, 1) from the top 52 bits: (v + 1/2) 2^-52 needs 53 significant
-// bits, so it is exact, and lies in [2^-53, 1 - 2^-53].  (A 53-bit v would round v + 1/2 up to
-// 2^53 for v = 2^53 - 1, i.e. u = 1 and log u = 0 -> rsq(-0) = -inf -> a NaN sample.)
-__device__ __forceinline__ double uniform52(uint32_t hi, uint32_t lo) {
-  const uint64_t v = (static_cast<uint64_t>(hi) << 32 | lo) >> 12;
-  return (static_cast<double>(v) + 0.5) * 0x1.0p-52;
+// Uniform in the open interval (0, 1) from a 32-bit word: (x + 1/2) 2^-32 has at most 33
+// significant bits, so it is exact, and lies in [2^-33, 1 - 2^-33] (never 0 or 1).
+__device__ __forceinline__ double uniform32(uint32_t x) {
+  return fma(static_cast<double>(x), 0x1.0p-32, 0x1.0p-33);
 }
 
-// log(x) for 0 < x <= 1 (normal).  x = m 2^e with m in [sqrt(1/2), sqrt(2)); f = m - 1 is exact;
-// log m = 2 atanh(s), s = f / (2 + f), summed as 2 s + s^3 P(s^2) with P the atanh series to s^21.
-__device__ __forceinline__ double log_unit(double x) {
-  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
-  int e = __builtin_amdgcn_frexp_exp(x);
-  const bool lo = m < 0.70710678118654752440;
-  m = lo ? m + m : m;
-  e = lo ? e - 1 : e;
-  const double f = m - 1.0;
-  const double d = 2.0 + f;  // in [1.7, 2.5]: a plain reciprocal + Newton division is exact enough
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(fma(-d, r, 1.0), r, r);
-  r = fma(fma(-d, r, 1.0), r, r);
-  double sq = f * r;
-  sq = fma(fma(-d, sq, f), r, sq);
-  const double z = sq * sq;
-  double p = 2.0 / 21.0;
-  p = fma_sc(p, z, 2.0 / 19.0);
-  p = fma_sc(p, z, 2.0 / 17.0);
-  p = fma_sc(p, z, 2.0 / 15.0);
-  p = fma_sc(p, z, 2.0 / 13.0);
-  p = fma_sc(p, z, 2.0 / 11.0);
-  p = fma_sc(p, z, 2.0 / 9.0);
-  p = fma_sc(p, z, 2.0 / 7.0);
-  p = fma_sc(p, z, 2.0 / 5.0);
-  p = fma_sc(p, z, 2.0 / 3.0);
-  const double logm = fma(sq * z, p, sq + sq);
+// log u for u = uniform32(x).  u = m 2^e, m in [1/2, 1); the top 7 mantissa bits, rounded, pick
+// the nearest centre c_k = 1/2 + k/128 (k = 0..64; c_64 = 1 exactly, so log u keeps its relative
+// accuracy as u -> 1); r = m (1/c_k) - 1 (one fma, |r| <= 1/128 + 2^-52);
+// log m = log1p(r) - log(1/c_k), log1p(r) = r + r^2 P(r), P to r^6 (next term < 2e-20).
+__device__ __forceinline__ double log_u32(uint32_t x) {
+  const double u = uniform32(x);
+  const double m = __builtin_amdgcn_frexp_mant(u);
+  const int e = __builtin_amdgcn_frexp_exp(u);
+  const int k = (((__double2hiint(m) >> 13) & 127) + 1) >> 1;
+  const double inv_c = kLogT[2 * k], neg_log_inv_c = kLogT[2 * k + 1];
+  const double r = fma(m, inv_c, -1.0);
+  double p = -1.0 / 8.0;
+  p = fma_sc(p, r, 1.0 / 7.0);
+  p = fma_sc(p, r, -1.0 / 6.0);
+  p = fma_sc(p, r, 1.0 / 5.0);
+  p = fma_sc(p, r, -1.0 / 4.0);
+  p = fma_sc(p, r, 1.0 / 3.0);
+  p = fma_sc(p, r, -1.0 / 2.0);
+  const double log1p_r = fma(r * r, p, r);
   constexpr double kLn2Hi = 0x1.62e42fefa3800p-1, kLn2Lo = 0x1.ef35793c76730p-45;
   const double de = static_cast<double>(e);
-  return fma(de, kLn2Hi, fma(de, kLn2Lo, logm));
+  return fma(de, kLn2Hi, fma(de, kLn2Lo, neg_log_inv_c + log1p_r));
 }
 
-// sqrt(-2 log u1).  The argument is >= 2^-52 (u1 <= 1 - 2^-53), never denormal, so rsq + two
-// Newton-Raphson steps (Goldschmidt form) replace the library sqrt and its rescaling.
-__device__ __forceinline__ double box_muller_radius(double u1) {
-  const double y = -2.0 * log_unit(u1);
+// sqrt(-2 log u).  The argument is >= 2^-33 ln 4 > 0, never denormal, so rsq + two Newton-Raphson
+// steps (Goldschmidt form) replace the library sqrt and its rescaling.
+__device__ __forceinline__ double box_muller_radius(uint32_t x) {
+  const double y = -2.0 * log_u32(x);
   double h = 0.5 * __builtin_amdgcn_rsq(y), r = y * (h + h);
   const double e = fma(-r, h, 0.5);
   r = fma(r, e, r);
@@ -117,37 +113,27 @@ __device__ __forceinline__ double box_muller_radius(double u1) {
   return fma(fma(-r, r, y), h, r);
 }
 
-// (cos, sin)(2 pi w / 2^64): quadrant q = round(w / 2^62) mod 4, remainder x = 2 pi (w - q 2^62) /
-// 2^64 in [-pi/4, pi/4) (53 significant bits of it kept), Taylor series to x^15 (sin) / x^16 (cos).
-__device__ __forceinline__ void cos_sin_turn(uint32_t whi, uint32_t wlo, double* cs, double* sn) {
-  const uint64_t w = static_cast<uint64_t>(whi) << 32 | wlo;
-  const uint32_t q = static_cast<uint32_t>((w + (uint64_t{1} << 61)) >> 62);
-  const int64_t rem = static_cast<int64_t>(w - (static_cast<uint64_t>(q) << 62)) >> 11;
-  constexpr double kTurn = 6.28318530717958647692 * 0x1.0p-53;
-  const double x = static_cast<double>(rem) * kTurn;
-  const double z = x * x;
-  double ps = -1.0 / 1307674368000.0;
-  ps = fma_sc(ps, z, 1.0 / 6227020800.0);
-  ps = fma_sc(ps, z, -1.0 / 39916800.0);
-  ps = fma_sc(ps, z, 1.0 / 362880.0);
-  ps = fma_sc(ps, z, -1.0 / 5040.0);
+// (cos, sin)(2 pi w / 2^32): table point k = round(w / 2^25) mod 128 (32-bit wrap-around), signed
+// remainder rem = w - k 2^25 in [-2^24, 2^24), b = 2 pi rem / 2^32 in [-pi/128, pi/128);
+// sin b = b + b^3 (-1/6 + b^2/120 - b^4/5040), cos b - 1 = b^2 (-1/2 + b^2/24 - b^4/720), and
+// (cos, sin)(a + b) = (C (1 + cm1) - S sb, S (1 + cm1) + C sb) with (C, S) = kTurn[k].
+__device__ __forceinline__ void cos_sin_u32(uint32_t w, double* cs, double* sn) {
+  const uint32_t k = (w + (1u << 24)) >> 25;
+  const int32_t rem = static_cast<int32_t>(w - (k << 25));
+  constexpr double kTurn32 = 6.28318530717958647692 * 0x1.0p-32;
+  const double b = static_cast<double>(rem) * kTurn32;
+  const double z = b * b;
+  double ps = -1.0 / 5040.0;
   ps = fma_sc(ps, z, 1.0 / 120.0);
   ps = fma_sc(ps, z, -1.0 / 6.0);
-  const double s = fma(x * z, ps, x);
-  double pc = 1.0 / 20922789888000.0;
-  pc = fma_sc(pc, z, -1.0 / 87178291200.0);
-  pc = fma_sc(pc, z, 1.0 / 479001600.0);
-  pc = fma_sc(pc, z, -1.0 / 3628800.0);
-  pc = fma_sc(pc, z, 1.0 / 40320.0);
-  pc = fma_sc(pc, z, -1.0 / 720.0);
+  const double sb = fma(b * z, ps, b);
+  double pc = -1.0 / 720.0;
   pc = fma_sc(pc, z, 1.0 / 24.0);
   pc = fma_sc(pc, z, -0.5);
-  const double c = fma(z, pc, 1.0);
-  // theta = q pi/2 + x: q=0 (c, s), 1 (-s, c), 2 (-c, -s), 3 (s, -c)
-  const bool swap = q & 1;
-  const double a = swap ? s : c, b = swap ? c : s;
-  *cs = ((q + 1) & 2) ? -a : a;
-  *sn = (q & 2) ? -b : b;
+  const double cm1 = z * pc;
+  const double C = kTurn[2 * k], S = kTurn[2 * k + 1];
+  *cs = fma(C, cm1, fma(-S, sb, C));
+  *sn = fma(S, cm1, fma(C, sb, S));
 }
 
 // Units [u0, u0 + count) of the global [O, T] grid (u = o T + t); unit u is written at
@@ -164,7 +150,18 @@ struct SampleArgs {
   int64_t so, st, sn;
 };
 
+// one sample: nominal + L z, written at p (16-B store when the pair is packed and aligned)
+__device__ __forceinline__ void put_sample(double* p, int64_t sn, double x, double y) {
+  if (sn == 2 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    *reinterpret_cast<double2*>(p) = make_double2(x, y);
+  } else {
+    p[0] = x;
+    p[1] = y;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
+  const int64_t pairs = (a.N + 1) >> 1;  // Philox calls per unit
   for (int64_t k = blockIdx.y; k < a.count; k += gridDim.y) {
     const int64_t u = a.u0 + k;
     const int64_t o = u / a.T, t = u - o * a.T;
@@ -172,30 +169,30 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
     const double nx = nom[0], ny = nom[1];
     double* dst = a.out + (o - a.o0) * a.so + (t - a.t0) * a.st;
     const bool noise = !(a.zero_first && t == 0);
-    const int64_t base = (static_cast<int64_t>(blockIdx.x) * kBlock * kPerThread) + threadIdx.x;
+    const int64_t base = (static_cast<int64_t>(blockIdx.x) * kBlock * kPairs) + threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < kPerThread; ++q) {
-      const int64_t i = base + q * kBlock;
-      if (i >= a.N) break;
-      double x = nx, y = ny;
+    for (int q = 0; q < kPairs; ++q) {
+      const int64_t pidx = base + q * kBlock;
+      if (pidx >= pairs) break;
+      const int64_t i = 2 * pidx;
+      double x0 = nx, y0 = ny, x1 = nx, y1 = ny;
       if (noise) {
-        const uint64_t g = static_cast<uint64_t>(u) * static_cast<uint64_t>(a.N) + static_cast<uint64_t>(i);
+        const uint64_t g = static_cast<uint64_t>(u) * static_cast<uint64_t>(pairs) + static_cast<uint64_t>(pidx);
         const Philox r = philox4x32_10(static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
                                        a.s0, a.s1, a.k0, a.k1);
-        const double rad = box_muller_radius(uniform52(r.x[0], r.x[1]));
-        double sn, cs;
-        cos_sin_turn(r.x[2], r.x[3], &cs, &sn);
-        const double z0 = rad * cs, z1 = rad * sn;
-        x = nx + a.l00 * z0;
-        y = ny + (a.l10 * z0 + a.l11 * z1);
+        double c0, s0, c1, s1;
+        const double rad0 = box_muller_radius(r.x[0]);
+        cos_sin_u32(r.x[1], &c0, &s0);
+        const double rad1 = box_muller_radius(r.x[2]);
+        cos_sin_u32(r.x[3], &c1, &s1);
+        const double z00 = rad0 * c0, z01 = rad0 * s0, z10 = rad1 * c1, z11 = rad1 * s1;
+        x0 = nx + a.l00 * z00;
+        y0 = ny + (a.l10 * z00 + a.l11 * z01);
+        x1 = nx + a.l00 * z10;
+        y1 = ny + (a.l10 * z10 + a.l11 * z11);
       }
-      double* p = dst + i * a.sn;
-      if (a.sn == 2 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-        *reinterpret_cast<double2*>(p) = make_double2(x, y);
-      } else {
-        p[0] = x;
-        p[1] = y;
-      }
+      put_sample(dst + i * a.sn, a.sn, x0, y0);
+      if (i + 1 < a.N) put_sample(dst + (i + 1) * a.sn, a.sn, x1, y1);
     }
   }
 }
@@ -238,8 +235,8 @@ int launch_samples(const double* nominal, int64_t n_obstacles, int64_t n_steps, 
   a.so = so;
   a.st = st;
   a.sn = sn;
-  const int64_t per_block = int64_t{kBlock} * kPerThread;
-  const int64_t gx = (n_samples + per_block - 1) / per_block;
+  const int64_t per_block = int64_t{kBlock} * kPairs;  // pairs per workgroup
+  const int64_t gx = ((n_samples + 1) / 2 + per_block - 1) / per_block;
   if (gx > 0x7fffffffLL) return DRCVAR_ERR_UNSUPPORTED;
   const unsigned gy = static_cast<unsigned>(count < 65535 ? count : 65535);
   (void)hipGetLastError();

@@ -14,9 +14,9 @@
  *   drcvar_sample_units_f64          the same draws for a contiguous block of (obstacle, step)
  *                                    units of a global batch (one rank's shard).
  *
- * Random numbers: Philox4x32-10 (counter-based; key = seed, counter = (sample index, stream)),
- * one call per sample -> a 52-bit uniform and a 64-bit turn -> Box-Muller -> z ~ N(0, I2); sample = nominal +
- * L z with L the lower Cholesky factor of noise_cov.  Same distribution as the reference's
+ * Random numbers: Philox4x32-10 (counter-based; key = seed, counter = (unit * ceil(N/2) + pair,
+ * stream)), one call per PAIR of samples of a unit -> two (32-bit uniform, 32-bit turn) pairs ->
+ * Box-Muller -> z ~ N(0, I2); sample = nominal + L z with L the lower Cholesky factor of noise_cov.  Same distribution as the reference's
  * np.random.multivariate_normal, not the same stream (numpy's MT19937 is sequential; the host
  * mirror in simulation/obstacles.py reproduces that stream exactly).  Output is a pure function
  * of (seed, stream_offset, indices): deterministic and independent of the launch geometry.

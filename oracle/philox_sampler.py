@@ -7,21 +7,26 @@ kernel behind ``include/drcvar_sampling.h`` (``csrc/drcvar_sampling.hip``); it n
 NumPy restatement of the device obstacle-sample generator, which replaces the reference's host
 draws ``simulation/obstacles.py:43-77`` (``np.random.multivariate_normal(zeros(2), noise_cov)`` per
 sample and step, step 0 the nominal start, ``:63``).  The reference's stream (sequential MT19937)
-is not reproducible in parallel, so the device generator defines its own: for the sample with
-global index ``g = (o * T + t) * N + i``
+is not reproducible in parallel, so the device generator defines its own: for the sample pair
+``(2p, 2p + 1)`` of unit ``u = o * T + t`` (``P = ceil(N / 2)`` pairs per unit)
 
 * Philox4x32-10 (Salmon et al., SC'11; multipliers 0xD2511F53 / 0xCD9E8D57, Weyl key increments
-  0x9E3779B9 / 0xBB67AE85) on counter ``(g lo, g hi, stream lo, stream hi)`` and key ``seed``;
-* ``u1 = ((x0:x1) >> 12 + 1/2) / 2^52`` in (0, 1) (exact); angle ``2 pi (x2:x3) / 2^64``;
+  0x9E3779B9 / 0xBB67AE85) on counter ``(g lo, g hi, stream lo, stream hi)``, ``g = u * P + p``,
+  and key ``seed`` -> words ``x0..x3``;
+* sample 2p from ``(x0, x1)``, sample 2p + 1 from ``(x2, x3)``: ``u1 = (x + 1/2) / 2^32`` in (0, 1)
+  (exact), angle ``2 pi w / 2^32``;
 * Box-Muller ``z = sqrt(-2 log u1) (cos, sin)``; sample ``nominal + L z``.
 
-``log_unit`` and ``cos_sin_turn`` restate the kernel's own series (atanh series of
-``s = f / (2 + f)``; quadrant from the top bits, Taylor series on [-pi/4, pi/4]) so the tests can
-check them against numpy's ``log`` / ``cos`` / ``sin`` and the kernel against this mirror.  The
-kernel contracts its polynomial steps into FMAs; numpy rounds each product, so the two agree to a
-few ulp, not bit for bit.
+``log_u32`` and ``cos_sin_u32`` restate the kernel's table-driven forms (65 mantissa centres +
+log1p series; 128 table angles + short sin / cos series) with the kernel's own tables, read from
+``csrc/drcvar_sampling_tables.inc``, so the tests can check them against extended-precision
+references and the kernel against this mirror.  The kernel contracts its polynomial steps into
+FMAs; numpy rounds each product, so the two agree to a few ulp, not bit for bit.
 """
 from __future__ import annotations
+
+import os
+import re
 
 import numpy as np
 
@@ -43,50 +48,65 @@ def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
     return c0, c1, c2, c3
 
 
-def uniform52(hi, lo):
-    """(top 52 bits + 1/2) / 2^52: exact, in [2^-53, 1 - 2^-53] (the kernel's ``uniform52``)."""
-    v = ((hi << np.uint64(32)) | lo) >> np.uint64(12)
-    return (v.astype(np.float64) + 0.5) * 2.0 ** -52
+_TABLES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd", "csrc",
+                       "drcvar_sampling_tables.inc")
 
 
-def log_unit(x):
-    """log x for 0 < x <= 1, the kernel's series (``log_unit``)."""
-    m, e = np.frexp(np.asarray(x, dtype=np.float64))
-    lo = m < 0.70710678118654752440
-    m = np.where(lo, m + m, m)
-    e = np.where(lo, e - 1, e).astype(np.float64)
-    f = m - 1.0
-    s = f / (2.0 + f)
-    z = s * s
-    p = np.full_like(z, 2.0 / 21.0)
-    for k in (19, 17, 15, 13, 11, 9, 7, 5, 3):
-        p = p * z + 2.0 / k
-    logm = (s * z) * p + (s + s)
+def _read_tables():
+    """kTurn [128, 2] (cos, sin of 2 pi k / 128) and kLogT [65, 2] (1/c_k, -log(1/c_k)) from the
+    kernel's generated table file (hex-float literals: exact bits)."""
+    tabs, cur = {}, None
+    with open(_TABLES) as f:
+        for line in f:
+            m = re.match(r"__constant__ double (\w+)\[", line)
+            if m:
+                cur = tabs.setdefault(m.group(1), [])
+            elif cur is not None and line.strip().startswith(("0x", "-0x")):
+                cur.extend(float.fromhex(v) for v in line.replace(",", " ").split())
+    return (np.array(tabs["kTurn"]).reshape(128, 2), np.array(tabs["kLogT"]).reshape(65, 2))
+
+
+TURN, LOGT = _read_tables()
+
+
+def uniform32(x):
+    """(x + 1/2) / 2^32 for 32-bit words: exact, in [2^-33, 1 - 2^-33] (the kernel's ``uniform32``)."""
+    return np.asarray(x, dtype=np.uint64).astype(np.float64) * 2.0 ** -32 + 2.0 ** -33
+
+
+def log_u32(x):
+    """log uniform32(x), the kernel's table-driven form (``log_u32``)."""
+    m, e = np.frexp(uniform32(x))
+    k = ((((m.view(np.uint64) >> np.uint64(45)) & np.uint64(127)) + np.uint64(1)) >> np.uint64(1)).astype(np.int64)
+    # the kernel's fma(m, 1/c_k, -1): the product kept in extended precision before the rounding
+    r = (m.astype(np.longdouble) * LOGT[k, 0].astype(np.longdouble) - 1).astype(np.float64)
+    p = np.full_like(r, -1.0 / 8.0)
+    for c in (1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0):
+        p = p * r + c
+    log1p_r = (r * r) * p + r
     ln2_hi, ln2_lo = float.fromhex("0x1.62e42fefa3800p-1"), float.fromhex("0x1.ef35793c76730p-45")
-    return e * ln2_hi + (e * ln2_lo + logm)
+    e = e.astype(np.float64)
+    return e * ln2_hi + (e * ln2_lo + (LOGT[k, 1] + log1p_r))
 
 
-def cos_sin_turn(whi, wlo):
-    """(cos, sin)(2 pi w / 2^64) for w = whi:wlo, the kernel's ``cos_sin_turn``."""
-    w = (np.asarray(whi, dtype=np.uint64) << np.uint64(32)) | np.asarray(wlo, dtype=np.uint64)
-    q = ((w + np.uint64(1 << 61)) >> np.uint64(62)).astype(np.uint64)
-    rem = (w - (q << np.uint64(62))).view(np.int64) >> np.int64(11)
-    x = rem.astype(np.float64) * (6.28318530717958647692 * 2.0 ** -53)
-    z = x * x
-    ps = np.full_like(z, -1.0 / 1307674368000.0)
-    for c in (1.0 / 6227020800.0, -1.0 / 39916800.0, 1.0 / 362880.0, -1.0 / 5040.0, 1.0 / 120.0,
-              -1.0 / 6.0):
+def cos_sin_u32(w):
+    """(cos, sin)(2 pi w / 2^32) for 32-bit words, the kernel's ``cos_sin_u32``."""
+    w = np.asarray(w, dtype=np.uint64) & _MASK32
+    k = (((w + np.uint64(1 << 24)) & _MASK32) >> np.uint64(25)).astype(np.int64)
+    rem = ((w - (k.astype(np.uint64) << np.uint64(25))) & _MASK32).astype(np.uint32).view(np.int32)
+    b = rem.astype(np.float64) * (6.28318530717958647692 * 2.0 ** -32)
+    z = b * b
+    ps = np.full_like(z, -1.0 / 5040.0)
+    for c in (1.0 / 120.0, -1.0 / 6.0):
         ps = ps * z + c
-    s = (x * z) * ps + x
-    pc = np.full_like(z, 1.0 / 20922789888000.0)
-    for c in (-1.0 / 87178291200.0, 1.0 / 479001600.0, -1.0 / 3628800.0, 1.0 / 40320.0,
-              -1.0 / 720.0, 1.0 / 24.0, -0.5):
+    sb = (b * z) * ps + b
+    pc = np.full_like(z, -1.0 / 720.0)
+    for c in (1.0 / 24.0, -0.5):
         pc = pc * z + c
-    c = z * pc + 1.0
-    q = q.astype(np.int64)
-    swap = (q & 1).astype(bool)
-    a, b = np.where(swap, s, c), np.where(swap, c, s)
-    return np.where((q + 1) & 2, -a, a), np.where(q & 2, -b, b)
+    cm1 = z * pc
+    C, S = TURN[k, 0], TURN[k, 1]
+    return C * cm1 + (-S * sb + C), S * cm1 + (C * sb + S)
 
 
 def sample_trajectories(nominal, n_samples: int, chol, seed: int, stream_offset: int = 0,
@@ -96,18 +116,23 @@ def sample_trajectories(nominal, n_samples: int, chol, seed: int, stream_offset:
     nominal = np.asarray(nominal, dtype=np.float64)
     O, T = nominal.shape[:2]
     l00, l10, l11 = chol
-    g = np.arange(O * T * n_samples, dtype=np.uint64)
+    P = (n_samples + 1) // 2
+    g = np.arange(O * T * P, dtype=np.uint64)            # unit-major: g = u * P + p
     x0, x1, x2, x3 = philox4x32_10(g & _MASK32, g >> np.uint64(32),
                                    np.uint64(stream_offset & 0xFFFFFFFF),
                                    np.uint64((stream_offset >> 32) & 0xFFFFFFFF),
                                    seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    rad = np.sqrt(-2.0 * log_unit(uniform52(x0, x1)))
-    cs, sn = cos_sin_turn(x2, x3)
-    z0, z1 = rad * cs, rad * sn
+    z = np.empty((O * T, 2 * P, 2))
+    for radw, angw, col in ((x0, x1, 0), (x2, x3, 1)):   # sample 2p from (x0, x1), 2p + 1 from (x2, x3)
+        rad = np.sqrt(-2.0 * log_u32(radw))
+        cs, sn = cos_sin_u32(angw)
+        z[:, col::2, 0] = (rad * cs).reshape(O * T, P)
+        z[:, col::2, 1] = (rad * sn).reshape(O * T, P)
+    z = z[:, :n_samples]
     out = np.empty((O, T, n_samples, 2))
-    nom = np.repeat(nominal.reshape(O * T, 1, 2), n_samples, axis=1).reshape(-1, 2)
-    out.reshape(-1, 2)[:, 0] = nom[:, 0] + l00 * z0
-    out.reshape(-1, 2)[:, 1] = nom[:, 1] + (l10 * z0 + l11 * z1)
+    nom = nominal.reshape(O * T, 1, 2)
+    out.reshape(O * T, n_samples, 2)[..., 0] = nom[..., 0] + l00 * z[..., 0]
+    out.reshape(O * T, n_samples, 2)[..., 1] = nom[..., 1] + (l10 * z[..., 0] + l11 * z[..., 1])
     if zero_first_step and T:
         out[:, 0] = nominal[:, 0, None, :]
     return out

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_DIR, OFFSET_TOL, load_golden
+from conftest import GOLDEN_DIR, OFFSET_TOL, REPO, load_golden
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.config.scenarios import get_scenario_config
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.simulation import obstacles as ob
 
@@ -65,36 +65,50 @@ def test_philox_mirror_known_answers(ctr, key, want):
 
 
 def test_sampler_series_accuracy():
-    """The kernel's log / cos / sin series (restated by the mirror) against long-double references:
-    log within 2 ulp over (0, 1), cos / sin of 2 pi w / 2^64 within 4e-16."""
+    """The kernel's table-driven log / cos / sin (restated by the mirror with the kernel's own
+    tables) against extended-precision references: log uniform32(x) within 2 ulp over every
+    kind of 32-bit word (u -> 1 included: the last mantissa centre is 1), cos / sin of
+    2 pi w / 2^32 within 2.5e-16."""
     from oracle import philox_sampler as ps
     rng = np.random.default_rng(3)
-    v = rng.integers(0, 2 ** 53, size=400_000, dtype=np.uint64)
-    u = np.concatenate([(v.astype(np.float64) + 0.5) * 2.0 ** -53,
-                        [2.0 ** -54, 1 - 2.0 ** -53, 2.0 ** -53, 0.5, 0.25, 0.7071067811865475, 0.7071067811865476]])
+    x = np.concatenate([rng.integers(0, 2 ** 32, size=1_000_000, dtype=np.uint64),
+                        np.array([0, 1, 2, 2 ** 31 - 1, 2 ** 31, 2 ** 32 - 2, 2 ** 32 - 1,
+                                  (2 ** 32 - 2 ** 24), 2 ** 25, 2 ** 24 - 1], dtype=np.uint64)])
+    u = ps.uniform32(x)
     ref = np.log(u.astype(np.longdouble))
     ulp = np.spacing(np.abs(ref.astype(np.float64)))
-    assert np.max(np.abs(ps.log_unit(u) - ref) / ulp) <= 2.0
-    w = np.concatenate([rng.integers(0, 2 ** 64 - 1, size=400_000, dtype=np.uint64, endpoint=True),
-                        np.array([0, 1 << 61, (1 << 61) - 1, 1 << 62, 3 << 62, 2 ** 64 - 1], dtype=np.uint64)])
-    c, s = ps.cos_sin_turn(w >> np.uint64(32), w & np.uint64(0xFFFFFFFF))
-    w53 = w & ~np.uint64(0x7FF)                   # the series sees the angle to 53 bits (rem >> 11)
+    assert np.max(np.abs(ps.log_u32(x) - ref) / ulp) <= 2.0
+    c, s = ps.cos_sin_u32(x)
     pi = np.longdouble("3.14159265358979323846264338327950288")
-    th = (w53.astype(np.longdouble) / np.longdouble(2.0 ** 64)) * (2 * pi)
-    assert np.max(np.abs(c - np.cos(th))) < 4e-16 and np.max(np.abs(s - np.sin(th))) < 4e-16
+    th = (x.astype(np.longdouble) / np.longdouble(2.0 ** 32)) * (2 * pi)
+    assert np.max(np.abs(c - np.cos(th))) < 2.5e-16 and np.max(np.abs(s - np.sin(th))) < 2.5e-16
     assert np.allclose(c * c + s * s, 1.0, atol=5e-16, rtol=0)
 
 
-def test_uniform_open_interval_extremes():
-    """ADVICE r1: the all-ones word must not map to u = 1 (log 1 = 0 -> a NaN Box-Muller radius);
-    the 52-bit uniform is exact and stays in [2^-53, 1 - 2^-53]."""
+def test_sampler_tables_are_the_generated_ones():
+    """csrc/drcvar_sampling_tables.inc holds exactly what scripts/gen_sampler_tables.py computes
+    (the kernel and the mirror read the same bits)."""
+    import importlib.util
     from oracle import philox_sampler as ps
-    ones, zero = np.array([0xFFFFFFFF], dtype=np.uint64), np.array([0], dtype=np.uint64)
-    hi = ps.uniform52(ones, ones)[0]
-    lo = ps.uniform52(zero, zero)[0]
-    assert hi == 1.0 - 2.0 ** -53 and lo == 2.0 ** -53
-    for u in (hi, lo):
-        r = np.sqrt(-2.0 * ps.log_unit(np.array([u])))[0]
+    spec = importlib.util.spec_from_file_location("gen", os.path.join(REPO, "scripts", "gen_sampler_tables.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    cs, sn = gen.turn_table()
+    inv, nl = gen.log_table()
+    np.testing.assert_array_equal(ps.TURN, np.stack([cs, sn], 1))
+    np.testing.assert_array_equal(ps.LOGT, np.stack([inv, nl], 1))
+    assert ps.LOGT[64, 0] == 1.0 and ps.LOGT[64, 1] == 0.0
+
+
+def test_uniform_open_interval_extremes():
+    """no word may map to u = 0 or 1 (log -> -inf / 0: an infinite or zero Box-Muller
+    radius); the 32-bit uniform is exact and stays in [2^-33, 1 - 2^-33]."""
+    from oracle import philox_sampler as ps
+    hi = ps.uniform32(np.array([0xFFFFFFFF], dtype=np.uint64))[0]
+    lo = ps.uniform32(np.array([0], dtype=np.uint64))[0]
+    assert hi == 1.0 - 2.0 ** -33 and lo == 2.0 ** -33
+    for w in (0, 0xFFFFFFFF):
+        r = np.sqrt(-2.0 * ps.log_u32(np.array([w], dtype=np.uint64)))[0]
         assert np.isfinite(r) and r > 0
 
 
