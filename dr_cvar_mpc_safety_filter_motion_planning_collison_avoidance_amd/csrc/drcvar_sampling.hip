@@ -35,7 +35,11 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kPairs = 2;  // sample pairs per thread (independent Philox calls for ILP)
+// Sample pairs per thread: two per iteration (independent Philox calls for ILP), kPairs in all.
+// A thread's work must outlast the wave launch: with 2 pairs per thread the waves lived ~4 k
+// cycles, the dispatcher kept only ~1.3 waves per SIMD resident and VALU was busy 52 % of the
+// kernel (rocprofv3 counters, profiles/r03/sampler_pmc_pairs2.json); 8 per thread keep the SIMDs fed.
+constexpr int kPairs = 8;
 
 #include "drcvar_sampling_tables.inc"
 
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
     double* dst = a.out + (o - a.o0) * a.so + (t - a.t0) * a.st;
     const bool noise = !(a.zero_first && t == 0);
     const int64_t base = (static_cast<int64_t>(blockIdx.x) * kBlock * kPairs) + threadIdx.x;
-#pragma unroll
+#pragma unroll 2
     for (int q = 0; q < kPairs; ++q) {
       const int64_t pidx = base + q * kBlock;
       if (pidx >= pairs) break;
