@@ -1492,16 +1492,20 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   // last wave gathers the scalars and checks the digests (lane = record).  (16-B loads of step
   // pairs, two halves of the records per wave, measured slower: the extra live registers spilled.)
   const double* base = cl.xbuf + half;
+#ifndef DRCVAR_CLUSTER_GATHER
+#define DRCVAR_CLUSTER_GATHER 8
+#endif
+  constexpr int kG = DRCVAR_CLUSTER_GATHER;  // agent-scope loads in flight per wave
   for (int q = wave; q < Q; q += kWaves) {
-    double v[8];
+    double v[kG];
     double t = op_identity(step_op);
-    for (int c0 = 0; c0 < cl.size; c0 += 8) {
+    for (int c0 = 0; c0 < cl.size; c0 += kG) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < kG; ++i)
         v[i] = c0 + i < cl.size ? load_wt(base + static_cast<int64_t>(c0 + i) * kRec + q * 64 + lane)
                                 : op_identity(step_op);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t = op_apply(step_op, t, v[i]);
+      for (int i = 0; i < kG; ++i) t = op_apply(step_op, t, v[i]);
     }
     s.red[q * 64 + lane] = t;
   }

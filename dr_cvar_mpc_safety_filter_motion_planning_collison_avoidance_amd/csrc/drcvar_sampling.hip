@@ -2,23 +2,28 @@
 //
 // Reference: simulation/obstacles.py:43-77 (generate_obstacle_sample_trajectories): for every step
 // t >= 1 the N samples are nominal[t] + N(0, noise_cov) (np.random.multivariate_normal), step 0 is
-// the nominal start for every sample (:63).  Here every PAIR of samples (2p, 2p + 1) of a unit is
-// one Philox4x32-10 call (counter = (unit * ceil(N/2) + p, stream), key = seed): its four 32-bit
-// words are two (radius, angle) uniform pairs -> Box-Muller -> L z, written straight into the
-// [O, T, N, 2] layout the halfspace kernel streams.
+// the nominal start for every sample (:63).  Here every PAIR of samples (p, p + P) of a unit,
+// P = ceil(N/2), is one Philox4x32-10 call (counter = (unit * P + p, stream), key = seed): its four
+// 32-bit words are two (radius, angle) uniform pairs -> Box-Muller -> L z, written straight into
+// the [O, T, N, 2] layout the halfspace kernel streams.  The pair's samples are half a unit apart so
+// that each of the two 16-B stores of a wave writes one contiguous 1 KB (pairs of adjacent samples
+// made every store instruction half-fill 16 cache lines: 0.76 ms per refill against 0.45 ms for the
+// arithmetic alone).
 //
 // The per-sample arithmetic bounds this kernel, not the 16-B store (round 2: 163 VALU instructions
-// per sample, 0.33 of HBM, VALU busy 1.02).  This form (round 3):
+// per sample, 0.33 of HBM, VALU busy 1.02).  This form (round 3, ~80 VALU per sample in the loop):
 //   * one Philox call per two samples (32-bit uniforms: radius up to 6.8 sd, angle resolution
-//     2^-32 turn) — half the 20 v_mad_u64_u32 + 20 v_bitop3_b32 per sample;
-//   * log u for u = (x + 1/2) 2^-32: frexp, the mantissa's top 7 bits (rounded) pick the nearest
-//     of 65 centres c_k (1/c_k and -log(1/c_k) in constant memory), r = m / c_k - 1 by one fma
-//     (|r| <= 1/128),
-//     log1p(r) to r^8 (truncation < 2e-20) — instead of a rcp/Newton division and a degree-21
-//     series;
-//   * cos / sin of 2 pi w / 2^32: the top 7 bits (rounded) pick the nearest of 128 table angles,
-//     the signed remainder |b| <= pi/128 goes through sin b to b^7 and cos b - 1 to b^6, rotated by
+//     2^-32 turn) — half the 20 v_mad_u64_u32 + 20 v_bitop3_b32 per sample; the round keys are
+//     bumped in SALU;
+//   * log u for u = (x + 1/2) 2^-32 = (2x + 1) 2^-33: frexp, the mantissa's top 9 bits (rounded)
+//     pick the nearest of 257 centres c_k, r = m / c_k - 1 by one fma (|r| <= 1/512),
+//     log1p(r) to r^6 — instead of a rcp/Newton division and a degree-21 series;
+//   * cos / sin of 2 pi w / 2^32: the top 9 bits (rounded) pick the nearest of 512 table angles,
+//     the signed remainder |b| <= pi/512 goes through sin b to b^5 and cos b - 1 to b^4, rotated by
 //     the table point — instead of a quadrant fold and series to x^15 / x^16;
+//   * both tables (12 KB) are copied to LDS per workgroup: a global table load would share vmcnt
+//     with the wave's earlier stores, and waiting for it waited for their write acknowledgements
+//     (0.678 -> 0.556 ms per C5 refill together with the packed 16-B store below);
 //   * sqrt through rsq + Newton (the argument is never denormal);
 //   * the series' Horner steps as v_fma_f64 with the coefficient in SGPRs (fma_sc).
 // The tables are generated once (scripts/gen_sampler_tables.py, extended precision, exact hex
@@ -61,8 +66,11 @@ __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32
     c1 = static_cast<uint32_t>(p1);
     c2 = n2;
     c3 = static_cast<uint32_t>(p0);
-    k0 += kW0;
-    k1 += kW1;
+    // The key schedule is bumped in SALU each round (volatile: otherwise all twenty round keys are
+    // hoisted out of the sample loop, spilled to VGPR lanes and read back with one v_readlane per
+    // use — VALU work in a VALU-bound kernel).
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(k0) : "s"(kW0) : "scc");
+    asm volatile("s_add_u32 %0, %0, %1" : "+s"(k1) : "s"(kW1) : "scc");
   }
   return Philox{{c0, c1, c2, c3}};
 }
@@ -76,26 +84,22 @@ __device__ __forceinline__ double fma_sc(double a, double b, double c) {
   return r;
 }
 
-// Uniform in the open interval (0, 1) from a 32-bit word: (x + 1/2) 2^-32 has at most 33
-// significant bits, so it is exact, and lies in [2^-33, 1 - 2^-33] (never 0 or 1).
-__device__ __forceinline__ double uniform32(uint32_t x) {
-  return fma(static_cast<double>(x), 0x1.0p-32, 0x1.0p-33);
-}
-
-// log u for u = uniform32(x).  u = m 2^e, m in [1/2, 1); the top 7 mantissa bits, rounded, pick
-// the nearest centre c_k = 1/2 + k/128 (k = 0..64; c_64 = 1 exactly, so log u keeps its relative
-// accuracy as u -> 1); r = m (1/c_k) - 1 (one fma, |r| <= 1/128 + 2^-52);
-// log m = log1p(r) - log(1/c_k), log1p(r) = r + r^2 P(r), P to r^6 (next term < 2e-20).
-__device__ __forceinline__ double log_u32(uint32_t x) {
-  const double u = uniform32(x);
-  const double m = __builtin_amdgcn_frexp_mant(u);
-  const int e = __builtin_amdgcn_frexp_exp(u);
-  const int k = (((__double2hiint(m) >> 13) & 127) + 1) >> 1;
-  const double inv_c = kLogT[2 * k], neg_log_inv_c = kLogT[2 * k + 1];
+// log u for the uniform u = (x + 1/2) 2^-32 in the open interval (0, 1) of a 32-bit word (at most
+// 33 significant bits: exact, in [2^-33, 1 - 2^-33], never 0 or 1).  It is formed as w = 2x + 1
+// (one fma with inline constants, exact) and u = w 2^-33, folded into the exponent.
+// u = m 2^e, m in [1/2, 1); the top 9 mantissa bits, rounded, pick the nearest centre
+// c_k = 1/2 + k/512 (k = 0..256; c_256 = 1 exactly, so log u keeps its relative accuracy as u -> 1);
+// r = m (1/c_k) - 1 (one fma, |r| <= 1/512 + 2^-52);
+// log m = log1p(r) - log(1/c_k), log1p(r) = r + r^2 P(r), P to r^4 (the next term, r^7 / 7, is
+// below 2^-56 of r).
+__device__ __forceinline__ double log_u32(uint32_t x, const double* log_t) {
+  const double w = fma(static_cast<double>(x), 2.0, 1.0);
+  const double m = __builtin_amdgcn_frexp_mant(w);
+  const int e = __builtin_amdgcn_frexp_exp(w) - 33;
+  const int k = (((__double2hiint(m) >> 11) & 511) + 1) >> 1;
+  const double inv_c = log_t[2 * k], neg_log_inv_c = log_t[2 * k + 1];
   const double r = fma(m, inv_c, -1.0);
-  double p = -1.0 / 8.0;
-  p = fma_sc(p, r, 1.0 / 7.0);
-  p = fma_sc(p, r, -1.0 / 6.0);
+  double p = -1.0 / 6.0;
   p = fma_sc(p, r, 1.0 / 5.0);
   p = fma_sc(p, r, -1.0 / 4.0);
   p = fma_sc(p, r, 1.0 / 3.0);
@@ -108,34 +112,32 @@ __device__ __forceinline__ double log_u32(uint32_t x) {
 
 // sqrt(-2 log u).  The argument is >= 2^-33 ln 4 > 0, never denormal, so rsq + two Newton-Raphson
 // steps (Goldschmidt form) replace the library sqrt and its rescaling.
-__device__ __forceinline__ double box_muller_radius(uint32_t x) {
-  const double y = -2.0 * log_u32(x);
-  double h = 0.5 * __builtin_amdgcn_rsq(y), r = y * (h + h);
+__device__ __forceinline__ double box_muller_radius(uint32_t x, const double* log_t) {
+  const double y = -2.0 * log_u32(x, log_t);
+  const double rs = __builtin_amdgcn_rsq(y);
+  double h = 0.5 * rs, r = y * rs;
   const double e = fma(-r, h, 0.5);
   r = fma(r, e, r);
   h = fma(h, e, h);
   return fma(fma(-r, r, y), h, r);
 }
 
-// (cos, sin)(2 pi w / 2^32): table point k = round(w / 2^25) mod 128 (32-bit wrap-around), signed
-// remainder rem = w - k 2^25 in [-2^24, 2^24), b = 2 pi rem / 2^32 in [-pi/128, pi/128);
-// sin b = b + b^3 (-1/6 + b^2/120 - b^4/5040), cos b - 1 = b^2 (-1/2 + b^2/24 - b^4/720), and
-// (cos, sin)(a + b) = (C (1 + cm1) - S sb, S (1 + cm1) + C sb) with (C, S) = kTurn[k].
-__device__ __forceinline__ void cos_sin_u32(uint32_t w, double* cs, double* sn) {
-  const uint32_t k = (w + (1u << 24)) >> 25;
-  const int32_t rem = static_cast<int32_t>(w - (k << 25));
+// (cos, sin)(2 pi w / 2^32): table point k = round(w / 2^23) mod 512 (32-bit wrap-around), signed
+// remainder rem = w - k 2^23 in [-2^22, 2^22), b = 2 pi rem / 2^32 in [-pi/512, pi/512);
+// sin b = b + b^3 (-1/6 + b^2/120) (next term b^7/5040: 1e-17 of b), cos b - 1 = b^2 (-1/2 + b^2/24)
+// (next term b^6/720 < 8e-17), and (cos, sin)(a + b) = (C (1 + cm1) - S sb, S (1 + cm1) + C sb)
+// with (C, S) = kTurn[k].
+__device__ __forceinline__ void cos_sin_u32(uint32_t w, const double* turn, double* cs, double* sn) {
+  const uint32_t k = (w + (1u << 22)) >> 23;
+  const int32_t rem = static_cast<int32_t>(w - (k << 23));
   constexpr double kTurn32 = 6.28318530717958647692 * 0x1.0p-32;
   const double b = static_cast<double>(rem) * kTurn32;
   const double z = b * b;
-  double ps = -1.0 / 5040.0;
-  ps = fma_sc(ps, z, 1.0 / 120.0);
-  ps = fma_sc(ps, z, -1.0 / 6.0);
+  const double ps = fma_sc(z, 1.0 / 120.0, -1.0 / 6.0);
   const double sb = fma(b * z, ps, b);
-  double pc = -1.0 / 720.0;
-  pc = fma_sc(pc, z, 1.0 / 24.0);
-  pc = fma_sc(pc, z, -0.5);
+  const double pc = fma_sc(z, 1.0 / 24.0, -0.5);
   const double cm1 = z * pc;
-  const double C = kTurn[2 * k], S = kTurn[2 * k + 1];
+  const double C = turn[2 * k], S = turn[2 * k + 1];
   *cs = fma(C, cm1, fma(-S, sb, C));
   *sn = fma(S, cm1, fma(C, sb, S));
 }
@@ -154,17 +156,40 @@ struct SampleArgs {
   int64_t so, st, sn;
 };
 
-// one sample: nominal + L z, written at p (16-B store when the pair is packed and aligned)
-__device__ __forceinline__ void put_sample(double* p, int64_t sn, double x, double y) {
-  if (sn == 2 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-    *reinterpret_cast<double2*>(p) = make_double2(x, y);
+// one sample: nominal + L z, written at p.  kPacked (sample stride 2 and every sample 16-B
+// aligned, decided once on the host): one 16-B store of a two-double vector — a branch per store
+// let the compiler sink the common first double out of both arms and split the 16-B store into two
+// 8-B ones.  kNT: nontemporal stores, for batches larger than the 256 MB MALL (the halfspace kernel
+// reads them back from HBM anyway): 0.536-0.552 -> 0.531-0.536 ms per C5 refill
+// (scripts/micro/gpu_samp_nt.sh); a cache-sized batch keeps ordinary stores, which its consumer
+// finds in the MALL.
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+template <bool kPacked, bool kNT>
+__device__ __forceinline__ void put_sample(double* p, double x, double y) {
+  if constexpr (kPacked) {
+    dbl2 v = {x, y};
+    if constexpr (kNT)
+      __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(p));
+    else
+      *reinterpret_cast<dbl2*>(p) = v;
   } else {
     p[0] = x;
     p[1] = y;
   }
 }
 
+template <bool kPacked, bool kNT>
 __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
+  // The tables are read from LDS, not from global memory: a global table load is counted by
+  // vmcnt together with the wave's earlier sample stores, and waiting for the load (in order)
+  // would wait for those stores' write acknowledgements too, serialising arithmetic and stores.
+  constexpr int kTurnLen = sizeof(kTurn) / sizeof(double), kLogLen = sizeof(kLogT) / sizeof(double);
+  __shared__ double s_turn[kTurnLen], s_log[kLogLen];
+  for (int i = threadIdx.x; i < kTurnLen + kLogLen; i += kBlock) {
+    if (i < kTurnLen) s_turn[i] = kTurn[i];
+    else s_log[i - kTurnLen] = kLogT[i - kTurnLen];
+  }
+  __syncthreads();
   const int64_t pairs = (a.N + 1) >> 1;  // Philox calls per unit
   for (int64_t k = blockIdx.y; k < a.count; k += gridDim.y) {
     const int64_t u = a.u0 + k;
@@ -172,31 +197,42 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
     const double* nom = a.nominal + o * a.nom_so + t * a.nom_st;
     const double nx = nom[0], ny = nom[1];
     double* dst = a.out + (o - a.o0) * a.so + (t - a.t0) * a.st;
-    const bool noise = !(a.zero_first && t == 0);
+    const int64_t sn = kPacked ? 2 : a.sn;
     const int64_t base = (static_cast<int64_t>(blockIdx.x) * kBlock * kPairs) + threadIdx.x;
+    if (a.zero_first && t == 0) {  // the noise-free first step: every sample is the nominal point
+#pragma unroll 1
+      for (int q = 0; q < kPairs; ++q) {
+        const int64_t pidx = base + q * kBlock;
+        if (pidx >= pairs) break;
+        put_sample<kPacked, kNT>(dst + pidx * sn, nx, ny);
+        if (pidx + pairs < a.N) put_sample<kPacked, kNT>(dst + (pidx + pairs) * sn, nx, ny);
+      }
+      continue;
+    }
+    const uint64_t g0 = static_cast<uint64_t>(u) * static_cast<uint64_t>(pairs) + static_cast<uint64_t>(base);
 #pragma unroll 2
     for (int q = 0; q < kPairs; ++q) {
       const int64_t pidx = base + q * kBlock;
       if (pidx >= pairs) break;
-      const int64_t i = 2 * pidx;
-      double x0 = nx, y0 = ny, x1 = nx, y1 = ny;
-      if (noise) {
-        const uint64_t g = static_cast<uint64_t>(u) * static_cast<uint64_t>(pairs) + static_cast<uint64_t>(pidx);
-        const Philox r = philox4x32_10(static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
-                                       a.s0, a.s1, a.k0, a.k1);
-        double c0, s0, c1, s1;
-        const double rad0 = box_muller_radius(r.x[0]);
-        cos_sin_u32(r.x[1], &c0, &s0);
-        const double rad1 = box_muller_radius(r.x[2]);
-        cos_sin_u32(r.x[3], &c1, &s1);
-        const double z00 = rad0 * c0, z01 = rad0 * s0, z10 = rad1 * c1, z11 = rad1 * s1;
-        x0 = nx + a.l00 * z00;
-        y0 = ny + (a.l10 * z00 + a.l11 * z01);
-        x1 = nx + a.l00 * z10;
-        y1 = ny + (a.l10 * z10 + a.l11 * z11);
-      }
-      put_sample(dst + i * a.sn, a.sn, x0, y0);
-      if (i + 1 < a.N) put_sample(dst + (i + 1) * a.sn, a.sn, x1, y1);
+      const uint64_t g = g0 + static_cast<uint64_t>(q * kBlock);
+      const Philox r = philox4x32_10(static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32),
+                                     a.s0, a.s1, a.k0, a.k1);
+      double c0, s0, c1, s1;
+      const double rad0 = box_muller_radius(r.x[0], s_log);
+      cos_sin_u32(r.x[1], s_turn, &c0, &s0);
+      const double rad1 = box_muller_radius(r.x[2], s_log);
+      cos_sin_u32(r.x[3], s_turn, &c1, &s1);
+      const double z00 = rad0 * c0, z01 = rad0 * s0, z10 = rad1 * c1, z11 = rad1 * s1;
+      const double x0 = nx + a.l00 * z00;
+      const double y0 = ny + (a.l10 * z00 + a.l11 * z01);
+      const double x1 = nx + a.l00 * z10;
+      const double y1 = ny + (a.l10 * z10 + a.l11 * z11);
+#ifdef DRCVAR_SAMPLER_NO_STORE  // diagnostic: the arithmetic alone (stores only for a sentinel)
+      if (x0 + y0 + x1 + y1 == 1234.5) put_sample<kPacked, kNT>(dst + pidx * sn, x0, y0);
+#else
+      put_sample<kPacked, kNT>(dst + pidx * sn, x0, y0);
+      if (pidx + pairs < a.N) put_sample<kPacked, kNT>(dst + (pidx + pairs) * sn, x1, y1);
+#endif
     }
   }
 }
@@ -244,8 +280,18 @@ int launch_samples(const double* nominal, int64_t n_obstacles, int64_t n_steps, 
   if (gx > 0x7fffffffLL) return DRCVAR_ERR_UNSUPPORTED;
   const unsigned gy = static_cast<unsigned>(count < 65535 ? count : 65535);
   (void)hipGetLastError();
-  hipLaunchKernelGGL(sample_kernel, dim3(static_cast<unsigned>(gx), gy), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), a);
+  const bool packed = sn == 2 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (so & 1) == 0 &&
+                      (st & 1) == 0;
+  constexpr int64_t kMallBytes = int64_t{256} << 20;
+  const bool nt = packed && count * n_samples * 16 > kMallBytes;
+  const dim3 grid(static_cast<unsigned>(gx), gy);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nt)
+    hipLaunchKernelGGL((sample_kernel<true, true>), grid, dim3(kBlock), 0, s, a);
+  else if (packed)
+    hipLaunchKernelGGL((sample_kernel<true, false>), grid, dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((sample_kernel<false, false>), grid, dim3(kBlock), 0, s, a);
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
 }
 

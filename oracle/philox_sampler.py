@@ -8,17 +8,17 @@ NumPy restatement of the device obstacle-sample generator, which replaces the re
 draws ``simulation/obstacles.py:43-77`` (``np.random.multivariate_normal(zeros(2), noise_cov)`` per
 sample and step, step 0 the nominal start, ``:63``).  The reference's stream (sequential MT19937)
 is not reproducible in parallel, so the device generator defines its own: for the sample pair
-``(2p, 2p + 1)`` of unit ``u = o * T + t`` (``P = ceil(N / 2)`` pairs per unit)
+``(p, p + P)`` of unit ``u = o * T + t`` (``P = ceil(N / 2)`` pairs per unit, ``p < P``)
 
 * Philox4x32-10 (Salmon et al., SC'11; multipliers 0xD2511F53 / 0xCD9E8D57, Weyl key increments
   0x9E3779B9 / 0xBB67AE85) on counter ``(g lo, g hi, stream lo, stream hi)``, ``g = u * P + p``,
   and key ``seed`` -> words ``x0..x3``;
-* sample 2p from ``(x0, x1)``, sample 2p + 1 from ``(x2, x3)``: ``u1 = (x + 1/2) / 2^32`` in (0, 1)
+* sample p from ``(x0, x1)``, sample p + P (if < N) from ``(x2, x3)``: ``u1 = (x + 1/2) / 2^32`` in (0, 1)
   (exact), angle ``2 pi w / 2^32``;
 * Box-Muller ``z = sqrt(-2 log u1) (cos, sin)``; sample ``nominal + L z``.
 
-``log_u32`` and ``cos_sin_u32`` restate the kernel's table-driven forms (65 mantissa centres +
-log1p series; 128 table angles + short sin / cos series) with the kernel's own tables, read from
+``log_u32`` and ``cos_sin_u32`` restate the kernel's table-driven forms (257 mantissa centres +
+log1p series; 512 table angles + short sin / cos series) with the kernel's own tables, read from
 ``csrc/drcvar_sampling_tables.inc``, so the tests can check them against extended-precision
 references and the kernel against this mirror.  The kernel contracts its polynomial steps into
 FMAs; numpy rounds each product, so the two agree to a few ulp, not bit for bit.
@@ -54,7 +54,7 @@ _TABLES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def _read_tables():
-    """kTurn [128, 2] (cos, sin of 2 pi k / 128) and kLogT [65, 2] (1/c_k, -log(1/c_k)) from the
+    """kTurn [512, 2] (cos, sin of 2 pi k / 512) and kLogT [257, 2] (1/c_k, -log(1/c_k)) from the
     kernel's generated table file (hex-float literals: exact bits)."""
     tabs, cur = {}, None
     with open(_TABLES) as f:
@@ -64,25 +64,26 @@ def _read_tables():
                 cur = tabs.setdefault(m.group(1), [])
             elif cur is not None and line.strip().startswith(("0x", "-0x")):
                 cur.extend(float.fromhex(v) for v in line.replace(",", " ").split())
-    return (np.array(tabs["kTurn"]).reshape(128, 2), np.array(tabs["kLogT"]).reshape(65, 2))
+    return (np.array(tabs["kTurn"]).reshape(-1, 2), np.array(tabs["kLogT"]).reshape(-1, 2))
 
 
 TURN, LOGT = _read_tables()
 
 
 def uniform32(x):
-    """(x + 1/2) / 2^32 for 32-bit words: exact, in [2^-33, 1 - 2^-33] (the kernel's ``uniform32``)."""
+    """(x + 1/2) / 2^32 for 32-bit words: exact, in [2^-33, 1 - 2^-33] (the kernel forms it as
+    (2x + 1) 2^-33, the scale folded into the exponent)."""
     return np.asarray(x, dtype=np.uint64).astype(np.float64) * 2.0 ** -32 + 2.0 ** -33
 
 
 def log_u32(x):
     """log uniform32(x), the kernel's table-driven form (``log_u32``)."""
     m, e = np.frexp(uniform32(x))
-    k = ((((m.view(np.uint64) >> np.uint64(45)) & np.uint64(127)) + np.uint64(1)) >> np.uint64(1)).astype(np.int64)
+    k = ((((m.view(np.uint64) >> np.uint64(43)) & np.uint64(511)) + np.uint64(1)) >> np.uint64(1)).astype(np.int64)
     # the kernel's fma(m, 1/c_k, -1): the product kept in extended precision before the rounding
     r = (m.astype(np.longdouble) * LOGT[k, 0].astype(np.longdouble) - 1).astype(np.float64)
-    p = np.full_like(r, -1.0 / 8.0)
-    for c in (1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0):
+    p = np.full_like(r, -1.0 / 6.0)
+    for c in (1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -1.0 / 2.0):
         p = p * r + c
     log1p_r = (r * r) * p + r
     ln2_hi, ln2_lo = float.fromhex("0x1.62e42fefa3800p-1"), float.fromhex("0x1.ef35793c76730p-45")
@@ -93,17 +94,13 @@ def log_u32(x):
 def cos_sin_u32(w):
     """(cos, sin)(2 pi w / 2^32) for 32-bit words, the kernel's ``cos_sin_u32``."""
     w = np.asarray(w, dtype=np.uint64) & _MASK32
-    k = (((w + np.uint64(1 << 24)) & _MASK32) >> np.uint64(25)).astype(np.int64)
-    rem = ((w - (k.astype(np.uint64) << np.uint64(25))) & _MASK32).astype(np.uint32).view(np.int32)
+    k = (((w + np.uint64(1 << 22)) & _MASK32) >> np.uint64(23)).astype(np.int64)
+    rem = ((w - (k.astype(np.uint64) << np.uint64(23))) & _MASK32).astype(np.uint32).view(np.int32)
     b = rem.astype(np.float64) * (6.28318530717958647692 * 2.0 ** -32)
     z = b * b
-    ps = np.full_like(z, -1.0 / 5040.0)
-    for c in (1.0 / 120.0, -1.0 / 6.0):
-        ps = ps * z + c
+    ps = z * (1.0 / 120.0) - 1.0 / 6.0
     sb = (b * z) * ps + b
-    pc = np.full_like(z, -1.0 / 720.0)
-    for c in (1.0 / 24.0, -0.5):
-        pc = pc * z + c
+    pc = z * (1.0 / 24.0) - 0.5
     cm1 = z * pc
     C, S = TURN[k, 0], TURN[k, 1]
     return C * cm1 + (-S * sb + C), S * cm1 + (C * sb + S)
@@ -123,11 +120,11 @@ def sample_trajectories(nominal, n_samples: int, chol, seed: int, stream_offset:
                                    np.uint64((stream_offset >> 32) & 0xFFFFFFFF),
                                    seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
     z = np.empty((O * T, 2 * P, 2))
-    for radw, angw, col in ((x0, x1, 0), (x2, x3, 1)):   # sample 2p from (x0, x1), 2p + 1 from (x2, x3)
+    for radw, angw, half in ((x0, x1, 0), (x2, x3, 1)):  # sample p from (x0, x1), p + P from (x2, x3)
         rad = np.sqrt(-2.0 * log_u32(radw))
         cs, sn = cos_sin_u32(angw)
-        z[:, col::2, 0] = (rad * cs).reshape(O * T, P)
-        z[:, col::2, 1] = (rad * sn).reshape(O * T, P)
+        z[:, half * P:(half + 1) * P, 0] = (rad * cs).reshape(O * T, P)
+        z[:, half * P:(half + 1) * P, 1] = (rad * sn).reshape(O * T, P)
     z = z[:, :n_samples]
     out = np.empty((O, T, n_samples, 2))
     nom = nominal.reshape(O * T, 1, 2)

@@ -1,0 +1,25 @@
+#!/usr/bin/env bash
+# build_variant.sh <name> <source-basename> <flags...>: the product library with one source
+# rebuilt with extra flags (the other sources from the cached objects of _native.build(); the MPC
+# source as its five parts, concurrently), written to scripts/micro/variants/<name>.so for
+# DRCVAR_DIAG_LIB runs.
+set -eu
+cd "$(dirname "$0")/../.."
+name=$1; src=$2; shift 2
+PKG=dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd
+mkdir -p scripts/micro/variants
+new=()
+if [ "$src" = drcvar_mpc ]; then
+  for k in 0 1 2 3 4; do
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -I include -DDRCVAR_MPC_PART=$k "$@" \
+      $PKG/csrc/$src.hip -o /tmp/variant_${name}_$k.o &
+    new+=(/tmp/variant_${name}_$k.o)
+  done
+  wait
+else
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -I include "$@" $PKG/csrc/$src.hip -o /tmp/variant_$name.o
+  new+=(/tmp/variant_$name.o)
+fi
+objs=$(ls $PKG/_lib/obj/*.o | grep -v "/$src.hip")
+hipcc --offload-arch=gfx950 -shared -fPIC $objs "${new[@]}" -o scripts/micro/variants/$name.so
+echo scripts/micro/variants/$name.so
