@@ -215,9 +215,9 @@ def timed(world, fn, dev, stream):
     res = fn()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if world > 1:  # (one rank: no barrier, so nothing can be pending for a second synchronize)
         dist.barrier()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     ev_s = ev0.elapsed_time(ev1) * 1e-3
     if world > 1:

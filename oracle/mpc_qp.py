@@ -258,6 +258,12 @@ def solve_qp(P, q, E, e, G, d, tol=1e-11, max_iter=80, n_diag_tail=0):
                 polished = True
                 status = "optimal"
                 break
+        if not polished:  # degenerate instances: primal-dual active-set steps from the IPM's guess
+            res = _polish_steps(P, q, E, e, G, d, lam > w)
+            if res is not None:
+                z, lam, nu = res
+                polished = True
+                status = "optimal"
     return z, lam, nu, {"status": status, "iterations": it, "merit": float(best[0]),
                         "polished": polished}
 
@@ -281,6 +287,42 @@ def _polish(P, q, E, e, G, d, active, feas_tol=1e-9):
     lam = np.zeros(G.shape[0])
     lam[active] = np.maximum(lam_a, 0.0)
     return z, lam, nu
+
+
+def _polish_steps(P, q, E, e, G, d, active, max_steps=40, feas_tol=1e-9):
+    """Active-set refinement when the guessed sets fail: solve the equality QP of the set, then
+    add the most violated inactive row or drop the active row with the most negative multiplier,
+    one row per step (a degenerate problem — more binding rows at a step than inputs — makes
+    moving every violated row at once cycle).  Returns (z, lam, nu) of the first set whose
+    solution is primal and dual feasible, else None."""
+    active = np.array(active, dtype=bool)
+    nz, me = P.shape[0], E.shape[0]
+    scale = 1.0 + np.abs(d).max(initial=0.0)
+    for _ in range(max_steps):
+        Ga = G[active]
+        K = sparse.bmat([[P, E.T, Ga.T], [E, None, None], [Ga, None, None]], format="csc")
+        try:
+            sol = splinalg.spsolve(K, np.concatenate([-q, e, d[active]]))
+        except RuntimeError:
+            return None
+        if not np.all(np.isfinite(sol)):
+            return None
+        z, nu, lam_a = sol[:nz], sol[nz:nz + me], sol[nz + me:]
+        viol = G @ z - d
+        viol[active] = -np.inf
+        worst_p = int(np.argmax(viol)) if viol.size else -1
+        worst_d = int(np.argmin(lam_a)) if lam_a.size else -1
+        p_bad = worst_p >= 0 and viol[worst_p] > feas_tol * scale
+        d_bad = worst_d >= 0 and lam_a[worst_d] < -feas_tol
+        if not p_bad and not d_bad:
+            lam = np.zeros(G.shape[0])
+            lam[active] = np.maximum(lam_a, 0.0)
+            return z, lam, nu
+        if p_bad:
+            active[worst_p] = True
+        else:
+            active[np.flatnonzero(active)[worst_d]] = False
+    return None
 
 
 def kkt_residuals(qp, z, lam, nu):

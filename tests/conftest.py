@@ -19,10 +19,10 @@ def pytest_configure(config):
 
 
 def golden_files():
-    """Halfspace fixtures (the mpc_*.npz hand-off fixtures are loaded by tests/test_mpc.py, the
-    singleton_*.npz call sequences by tests/test_singletons.py)."""
+    """Halfspace fixtures (the mpc_*.npz hand-off fixtures and the qp_*.npz QP instances are loaded
+    by tests/test_mpc.py, the singleton_*.npz call sequences by tests/test_singletons.py)."""
     return sorted(p for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not os.path.basename(p).startswith(("mpc_", "singleton_")))
+                  if not os.path.basename(p).startswith(("mpc_", "qp_", "singleton_")))
 
 
 def load_golden(path):

@@ -92,6 +92,28 @@ def test_oracle_reproduces_golden_with_kkt_certificate(path):
         assert abs(info["objective"] - z["objective"][m]) <= 1e-9 * abs(z["objective"][m])
 
 
+def _c5_degenerate():
+    z = load(os.path.join(GOLDEN_DIR, "qp_c5_degenerate.npz"))
+    rows = [np.concatenate([z["h"][:, t], z["g"][:, t, None]], -1) for t in range(z["h"].shape[1])]
+    return z, rows
+
+
+def test_oracle_polishes_the_degenerate_c5_handoff():
+    """bench.py's C5 hand-off of round 3 (tests/golden/make_golden_qp_c5.py): the oracle's IPM
+    stalls at merit ~4e-10 and its three guessed active sets fail; the one-row-per-step refinement
+    (mpc_qp._polish_steps) must find the exact answer (before it, the oracle returned an
+    OPTIMAL_INACCURATE iterate 2e-4 away from the device's better answer)."""
+    z, rows = _c5_degenerate()
+    A, B, C = double_integrator()
+    H = z["x_ref"].shape[0] - 1
+    x, u, info = mpc_qp.filter_trajectory(A, B, C, 2 * np.eye(4), np.eye(2), H, z["x0"], z["x_ref"],
+                                          None, rows, tuple(z["u_bounds"]), tuple(z["p_bounds"]))
+    assert info["status"] == "optimal" and info["polished"]
+    assert max(info["kkt"].values()) < 1e-9, info["kkt"]
+    np.testing.assert_allclose(u, z["u_expected"], atol=1e-9)
+    assert abs(info["objective"] - float(z["objective"])) <= 1e-12 * float(z["objective"])
+
+
 def test_oracle_without_constraints_is_the_lq_tracking_solution():
     A, B, C = double_integrator()
     H = 12
@@ -484,3 +506,26 @@ def test_gpu_c5_handoff_shape(dev):
                                           (np.full(2, -10.0), np.full(2, 10.0)))
     assert io["status"] == "optimal"
     np.testing.assert_allclose(u[0].cpu().numpy(), uo, atol=MPC_TOL)
+
+
+@pytest.mark.gpu
+def test_gpu_degenerate_c5_handoff_matches_polished_oracle(dev):
+    """The degenerate C5 hand-off (12 800 rows) on the clustered launch and on one workgroup: both
+    polished, within MPC_TOL of the oracle's KKT-certified answer, objective to 1e-9."""
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    z, _ = _c5_degenerate()
+    A, B, C = double_integrator()
+    H = z["x_ref"].shape[0] - 1
+    model = mf.MPCModel(A, B, C, 2 * np.eye(4), np.eye(2), H, tuple(z["u_bounds"]), tuple(z["p_bounds"]),
+                        device=dev)
+    Tt = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    for opts in (None, mf.make_options(cluster_size=1)):
+        x, u, info = mf.filter_batch(model, Tt(z["h"][None]), Tt(z["g"][None]), Tt(z["x0"][None]),
+                                     Tt(z["x_ref"][None]), Tt(np.zeros((1, H, 2))), options=opts)
+        info = info[0].cpu().numpy()
+        assert int(info[_native.MPC_INFO_STATUS]) == _native.MPC_STATUS_OPTIMAL, info
+        assert info[_native.MPC_INFO_POLISHED] == 1, info
+        np.testing.assert_allclose(u[0].cpu().numpy(), z["u_expected"], atol=MPC_TOL)
+        np.testing.assert_allclose(x[0].cpu().numpy(), z["x_expected"], atol=MPC_TOL)
+        assert abs(info[_native.MPC_INFO_OBJECTIVE] - float(z["objective"])) <= 1e-9 * float(z["objective"])
