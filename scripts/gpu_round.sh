@@ -23,6 +23,10 @@ for s in ${STEPS:-pytest smoke bench bench_c5 prof mpcprof pmc}; do
     bench_eager) step bench_eager 600 python bench.py --launch eager --no-large --no-cpu-baseline ;;
     bench_c5) step bench_c5 600 python bench.py --workload c5 --steps 200 --warmup 10 --graph-batch 10 --no-large --no-cpu-baseline ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 2000 --no-cpu-baseline ;;
+    prof20) step rocprof20 600 rocprofv3 --kernel-trace --stats -d $OUT/prof20 -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20) step bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    samppmc) step sampler_pmc 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/sampler_pmc -o run --output-format csv -- python3 scripts/micro/sampler_bench.py ;;
+    dist) step dist 900 bash scripts/gpu_dist.sh ;;
     mpcprof) step mpc_bench 300 rocprofv3 --kernel-trace --stats -d $OUT/mpcprof -o run --output-format csv -- python3 scripts/mpc_bench.py ;;
     pmc)
       for w in c3 c5; do
