@@ -33,6 +33,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "drcvar_sampling.h"
@@ -84,36 +85,41 @@ __device__ __forceinline__ double fma_sc(double a, double b, double c) {
   return r;
 }
 
-// log u for the uniform u = (x + 1/2) 2^-32 in the open interval (0, 1) of a 32-bit word (at most
-// 33 significant bits: exact, in [2^-33, 1 - 2^-33], never 0 or 1).  It is formed as w = 2x + 1
-// (one fma with inline constants, exact) and u = w 2^-33, folded into the exponent.
+// -2 log u for the uniform u = (x + 1/2) 2^-32 in the open interval (0, 1) of a 32-bit word (at
+// most 33 significant bits: exact, in [2^-33, 1 - 2^-33], never 0 or 1).  It is formed as
+// w = 2x + 1 (one fma with inline constants, exact) and u = w 2^-33, folded into the exponent.
 // u = m 2^e, m in [1/2, 1); the top 9 mantissa bits, rounded, pick the nearest centre
 // c_k = 1/2 + k/512 (k = 0..256; c_256 = 1 exactly, so log u keeps its relative accuracy as u -> 1);
-// r = m (1/c_k) - 1 (one fma, |r| <= 1/512 + 2^-52);
-// log m = log1p(r) - log(1/c_k), log1p(r) = r + r^2 P(r), P to r^4 (the next term, r^7 / 7, is
-// below 2^-56 of r).
-__device__ __forceinline__ double log_u32(uint32_t x, const double* log_t) {
+// r = m (1/c_k) - 1 (|r| <= 1/512 + 2^-52); log m = log1p(r) - log(1/c_k),
+// log1p(r) = r + r^2 P(r), P to r^4 (the next term, r^7 / 7, is below 2^-56 of r).
+// The factor -2 of Box-Muller is folded in exactly: the LDS table holds -2/c_k and 2 log(1/c_k)
+// (indexed by the 9 bits themselves, each centre stored for both of its indices), the fma gives
+// r2 = -2r, the Horner coefficients are those of P scaled by powers of two so that the sum is
+// -P/2 in r2, and -2 log1p(r) = r2 + r2^2 (-P/2).  Every step is the unscaled step times a power
+// of two, so the result is bitwise -2 times the unscaled evaluation (what the host mirror,
+// oracle/philox_sampler.py, computes) — one multiply less.
+__device__ __forceinline__ double neg2_log_u32(uint32_t x, const double* log_t) {
   const double w = fma(static_cast<double>(x), 2.0, 1.0);
   const double m = __builtin_amdgcn_frexp_mant(w);
   const int e = __builtin_amdgcn_frexp_exp(w) - 33;
-  const int k = (((__double2hiint(m) >> 11) & 511) + 1) >> 1;
-  const double inv_c = log_t[2 * k], neg_log_inv_c = log_t[2 * k + 1];
-  const double r = fma(m, inv_c, -1.0);
-  double p = -1.0 / 6.0;
-  p = fma_sc(p, r, 1.0 / 5.0);
-  p = fma_sc(p, r, -1.0 / 4.0);
-  p = fma_sc(p, r, 1.0 / 3.0);
-  p = fma_sc(p, r, -1.0 / 2.0);
-  const double log1p_r = fma(r * r, p, r);
+  const uint32_t idx = __builtin_amdgcn_ubfe(static_cast<uint32_t>(__double2hiint(m)), 11, 9);
+  const double ninv2 = log_t[2 * idx], log_inv2 = log_t[2 * idx + 1];  // -2/c_k, 2 log(1/c_k)
+  const double r2 = fma(m, ninv2, 2.0);                                 // -2 r
+  double q = (-1.0 / 6.0) * (-1.0 / 32.0);
+  q = fma_sc(q, r2, (1.0 / 5.0) * (1.0 / 16.0));
+  q = fma_sc(q, r2, (-1.0 / 4.0) * (-1.0 / 8.0));
+  q = fma_sc(q, r2, (1.0 / 3.0) * (1.0 / 4.0));
+  q = fma_sc(q, r2, (-1.0 / 2.0) * (-1.0 / 2.0));                     // -P(r) / 2
+  const double m2log1p = fma(r2 * r2, q, r2);                           // -2 log1p(r)
   constexpr double kLn2Hi = 0x1.62e42fefa3800p-1, kLn2Lo = 0x1.ef35793c76730p-45;
   const double de = static_cast<double>(e);
-  return fma(de, kLn2Hi, fma(de, kLn2Lo, neg_log_inv_c + log1p_r));
+  return fma(de, -2.0 * kLn2Hi, fma(de, -2.0 * kLn2Lo, log_inv2 + m2log1p));
 }
 
 // sqrt(-2 log u).  The argument is >= 2^-33 ln 4 > 0, never denormal, so rsq + two Newton-Raphson
 // steps (Goldschmidt form) replace the library sqrt and its rescaling.
 __device__ __forceinline__ double box_muller_radius(uint32_t x, const double* log_t) {
-  const double y = -2.0 * log_u32(x, log_t);
+  const double y = neg2_log_u32(x, log_t);
   const double rs = __builtin_amdgcn_rsq(y);
   double h = 0.5 * rs, r = y * rs;
   const double e = fma(-r, h, 0.5);
@@ -129,7 +135,7 @@ __device__ __forceinline__ double box_muller_radius(uint32_t x, const double* lo
 // with (C, S) = kTurn[k].
 __device__ __forceinline__ void cos_sin_u32(uint32_t w, const double* turn, double* cs, double* sn) {
   const uint32_t k = (w + (1u << 22)) >> 23;
-  const int32_t rem = static_cast<int32_t>(w - (k << 23));
+  const int32_t rem = __builtin_amdgcn_sbfe(static_cast<int32_t>(w), 0, 23);  // = w - k 2^23
   constexpr double kTurn32 = 6.28318530717958647692 * 0x1.0p-32;
   const double b = static_cast<double>(rem) * kTurn32;
   const double z = b * b;
@@ -183,11 +189,17 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
   // The tables are read from LDS, not from global memory: a global table load is counted by
   // vmcnt together with the wave's earlier sample stores, and waiting for the load (in order)
   // would wait for those stores' write acknowledgements too, serialising arithmetic and stores.
-  constexpr int kTurnLen = sizeof(kTurn) / sizeof(double), kLogLen = sizeof(kLogT) / sizeof(double);
-  __shared__ double s_turn[kTurnLen], s_log[kLogLen];
-  for (int i = threadIdx.x; i < kTurnLen + kLogLen; i += kBlock) {
-    if (i < kTurnLen) s_turn[i] = kTurn[i];
-    else s_log[i - kTurnLen] = kLogT[i - kTurnLen];
+  constexpr int kTurnLen = sizeof(kTurn) / sizeof(double);
+  constexpr int kLogIdx = 2 * (sizeof(kLogT) / sizeof(double) / 2 - 1);  // 512 nine-bit indices
+  __shared__ double s_turn[kTurnLen], s_log[2 * kLogIdx];
+  for (int i = threadIdx.x; i < kTurnLen + kLogIdx; i += kBlock) {
+    if (i < kTurnLen) {
+      s_turn[i] = kTurn[i];
+    } else {  // index j -> centre (j + 1) / 2, scaled by -2 (exact)
+      const int j = i - kTurnLen, c = (j + 1) >> 1;
+      s_log[2 * j] = -2.0 * kLogT[2 * c];
+      s_log[2 * j + 1] = -2.0 * kLogT[2 * c + 1];
+    }
   }
   __syncthreads();
   const int64_t pairs = (a.N + 1) >> 1;  // Philox calls per unit
@@ -278,7 +290,12 @@ int launch_samples(const double* nominal, int64_t n_obstacles, int64_t n_steps, 
   const int64_t per_block = int64_t{kBlock} * kPairs;  // pairs per workgroup
   const int64_t gx = ((n_samples + 1) / 2 + per_block - 1) / per_block;
   if (gx > 0x7fffffffLL) return DRCVAR_ERR_UNSUPPORTED;
-  const unsigned gy = static_cast<unsigned>(count < 65535 ? count : 65535);
+  // Workgroup rows loop over units (k += gridDim.y): up to four units per row once the grid has
+  // >= 8192 workgroups, so the per-workgroup LDS table copy (~4 % of the VALU work at one unit per
+  // row) is amortised; small batches keep one unit per row to fill the device.
+  int64_t rows = std::max((count + 3) / 4, (int64_t{8192} + gx - 1) / gx);
+  rows = std::min(rows, std::min(count, int64_t{65535}));
+  const unsigned gy = static_cast<unsigned>(rows);
   (void)hipGetLastError();
   const bool packed = sn == 2 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (so & 1) == 0 &&
                       (st & 1) == 0;
