@@ -235,10 +235,11 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
       const double rad1 = box_muller_radius(r.x[2], s_log);
       cos_sin_u32(r.x[3], s_turn, &c1, &s1);
       const double z00 = rad0 * c0, z01 = rad0 * s0, z10 = rad1 * c1, z11 = rad1 * s1;
-      const double x0 = nx + a.l00 * z00;
-      const double y0 = ny + (a.l10 * z00 + a.l11 * z01);
-      const double x1 = nx + a.l00 * z10;
-      const double y1 = ny + (a.l10 * z10 + a.l11 * z11);
+      // nominal + L z as an fma chain (the mirror rounds ny + (l10 z0 + l11 z1): a few ulp apart)
+      const double x0 = fma(a.l00, z00, nx);
+      const double y0 = fma(a.l10, z00, fma(a.l11, z01, ny));
+      const double x1 = fma(a.l00, z10, nx);
+      const double y1 = fma(a.l10, z10, fma(a.l11, z11, ny));
 #ifdef DRCVAR_SAMPLER_NO_STORE  // diagnostic: the arithmetic alone (stores only for a sentinel)
       if (x0 + y0 + x1 + y1 == 1234.5) put_sample<kPacked, kNT>(dst + pidx * sn, x0, y0);
 #else

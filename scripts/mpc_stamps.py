@@ -22,10 +22,15 @@ dev = torch.device("cuda", 0)
 lib = _native.lib()
 lib.drcvar_diag_mpc_stamps.argtypes = [ctypes.c_void_p]
 def npz_problem(path, key):
-    """A problem saved by scripts/micro/dump_bench_qps.py / dump_qp_problems.py (double integrator)."""
+    """A problem saved by scripts/micro/dump_bench_qps.py / dump_qp_problems.py (double integrator),
+    or, with key "fixture", a tests/golden/qp_*.npz fixture (h [O, H, 2], g, x0, x_ref)."""
     z = np.load(path)
-    h, g, x0, xr = (torch.as_tensor(z[f"{key}_{s}"]).to(dev) for s in ("h", "g", "x0", "xr"))
-    H = int(key.split("_")[0][1:])
+    if key == "fixture":
+        h, g, x0, xr = (torch.as_tensor(z[s][None]).to(dev) for s in ("h", "g", "x0", "x_ref"))
+        H = int(z["x_ref"].shape[0]) - 1
+    else:
+        h, g, x0, xr = (torch.as_tensor(z[f"{key}_{s}"]).to(dev) for s in ("h", "g", "x0", "xr"))
+        H = int(key.split("_")[0][1:])
     dt = 0.2
     A = np.block([[np.eye(2), dt * np.eye(2)], [np.zeros((2, 2)), np.eye(2)]])
     Bm = np.block([[0.5 * dt ** 2 * np.eye(2)], [dt * np.eye(2)]])
