@@ -210,8 +210,12 @@ def timed(world, fn, dev, stream):
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
+    # torch creates a HIP event on its first record: both are created here, ev0 recorded just
+    # before the wall clock starts and ev1 re-recorded after the last step (the first region of a
+    # process otherwise paid ~8 us of event creation inside it: scripts/micro/first_region.py)
+    ev1.record(stream)
     ev0.record(stream)
+    t0 = time.perf_counter()
     res = fn()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
