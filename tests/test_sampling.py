@@ -223,6 +223,27 @@ def test_device_sampler_unit_range_is_a_slice_of_the_batch(dev, O, T, N, begin, 
         assert bool((big[1::2] == -7.0).all())
 
 
+@pytest.mark.gpu
+def test_device_sampler_large_batch_paths(dev):
+    """A batch above the 256 MB MALL (12 800 units x 2 600 samples, 532 MB) takes the nontemporal
+    store path and workgroup rows that loop over several units; its values equal the ordinary path's
+    (small unit-range draws: packed stores, one unit per row) bit for bit, and the mirror's."""
+    import torch
+    from oracle import philox_sampler as ps
+    O, T, N = 256, 50, 2600
+    cov = np.array([[0.04, 0.012], [0.012, 0.02]])
+    nom = _nominal(dev, O, T)
+    whole = ob.sample_trajectories_device(nom, N, cov, seed=31, stream_offset=3)
+    flat = whole.reshape(O * T, N, 2)
+    for begin, count in ((0, 3), (4321, 5), (O * T - 4, 4)):
+        part = ob.sample_units_device(nom, N, begin, count, cov, seed=31, stream_offset=3)
+        assert torch.equal(part, flat[begin:begin + count]), (begin, count)
+    L = np.linalg.cholesky(cov)
+    want = ps.sample_trajectories(nom[:1].cpu().numpy(), N, (L[0, 0], L[1, 0], L[1, 1]), 31, 3, True)
+    np.testing.assert_allclose(whole[:1].cpu().numpy(), want, rtol=0, atol=1e-14)
+    del whole, flat
+
+
 def test_device_sampler_unit_range_validation():
     import torch
     if not torch.cuda.is_available():
