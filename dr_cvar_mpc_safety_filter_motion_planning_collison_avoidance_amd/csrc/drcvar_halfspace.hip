@@ -812,12 +812,16 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // The unit's direction input and the early scalars are fetched while the 16-B sample loads
   // are in flight (otherwise the compiler sinks these scalar loads to their first use, after
   // barrier 1, and their latency lands on the critical path).
+  // The pivot of the row-0 moments (the unit's first sample, a uniform scalar load) is issued in
+  // the same batch: loaded after the wait for the direction input, it put a second scalar-memory
+  // round trip in series on the way to the first moment sums.
   const double* dp = dir + o * dir_s_obs + t * dir_s_step;
   const double e0 = dp[0], e1 = dp[1];
+  const double px = base[0], py = base[1];  // pivot (uniform scalar load)
   const double inv_n = prm.inv_n, inv_n0 = prm.inv_n0, deg_sq = prm.degenerate_sq;
   const double z_lo = prm.z_lo, hist_scale = prm.hist_scale;
-  asm volatile("" ::"s"(e0), "s"(e1), "s"(inv_n), "s"(inv_n0), "s"(deg_sq), "s"(z_lo),
-               "s"(hist_scale));
+  asm volatile("" ::"s"(e0), "s"(e1), "s"(px), "s"(py), "s"(inv_n), "s"(inv_n0), "s"(deg_sq),
+               "s"(z_lo), "s"(hist_scale));
   // the histogram is cleared while the sample loads are in flight (barrier 1 orders it before
   // the first atomic)
 #pragma unroll
@@ -826,7 +830,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // row 0 only (the first BLOCK samples), shifted by the unit's first sample and summed in fp32 —
   // they merely position the fast-path window, so a subsample at low precision is enough: an
   // inaccurate window can only cost speed (the exact fallback), never exactness.
-  const double px = base[0], py = base[1];  // pivot (uniform scalar load)
   double mom[2] = {0.0, 0.0};               // Sx Sy
   float mom0[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // row 0, pivot-shifted: Sa Sb Saa Sbb Sab
 #pragma unroll
