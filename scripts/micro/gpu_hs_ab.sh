@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
-# C3 A/B: baseline library, product, kernarg-preload variant — the bench's metric line at K = 2000
-# and K = 20, interleaved; then the halfspace parity tests on the preload variant.
+# C3 A/B: a baseline library (scripts/micro/variants/hs_base.so) against the product, and a variant
+# (hs_preload.so) — the bench's metric line at K = 2000 and K = 20, interleaved; then the halfspace
+# parity tests on the variant.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
