@@ -494,6 +494,16 @@ __device__ __forceinline__ void append_candidate(double* region, uint32_t& wbase
   wbase += static_cast<uint32_t>(__popcll(ballot));
 }
 
+// Lane w < NW: the candidate count of wave w (0 elsewhere) — the ranking's input, read by the
+// caller so that it can be issued together with other LDS reads.
+template <int NW>
+__device__ __forceinline__ uint32_t wave_counts(const uint32_t* wcount, int lane) {
+  return lane < NW ? wcount[lane] : 0u;
+}
+// Makes a loaded value available at this point (an empty asm that consumes it): keeps the compiler
+// from sinking independent LDS loads past a branch or a wait, so they share one round trip.
+__device__ __forceinline__ void lds_values_ready(uint32_t v) { asm volatile("" ::"v"(v)); }
+
 // Wave 0 (all lanes active): tau = the candidate of rank rr among the c <= kCap candidates held in
 // per-wave regions cand[w * kCap + i], i < wcount[w] (global order: wave, then position — fixed).
 // Candidates are pulled into registers (g = lane, lane + 64) and compared through readlane, so
@@ -501,10 +511,8 @@ __device__ __forceinline__ void append_candidate(double* region, uint32_t& wbase
 // (cand - tau), accumulated in candidate order.  Q = candidate registers per lane: 1 when
 // c <= 64 (the usual case), 2 up to kCap.
 template <int NW, int Q>
-__device__ __forceinline__ double rank_candidates_q(const double* cand, const uint32_t* wcount,
-                                                    uint32_t c, uint32_t rr, int lane,
-                                                    double* s_cand) {
-  const uint32_t cw = lane < NW ? wcount[lane] : 0u;  // lane w < NW: count of wave w
+__device__ __forceinline__ double rank_candidates_q(const double* cand, uint32_t cw, uint32_t c,
+                                                    uint32_t rr, int lane, double* s_cand) {
   int slot[2] = {-1, -1};
   uint32_t acc = 0;
 #pragma unroll
@@ -562,12 +570,10 @@ __device__ __forceinline__ double rank_candidates_q(const double* cand, const ui
   return readlane_f64(found_v, src);
 }
 template <int NW>
-__device__ __forceinline__ double rank_candidates(const double* cand, const uint32_t* wcount,
-                                                  uint32_t c, uint32_t rr, int lane,
-                                                  double* s_cand) {
-  return c <= static_cast<uint32_t>(kWave)
-             ? rank_candidates_q<NW, 1>(cand, wcount, c, rr, lane, s_cand)
-             : rank_candidates_q<NW, 2>(cand, wcount, c, rr, lane, s_cand);
+__device__ __forceinline__ double rank_candidates(const double* cand, uint32_t cw, uint32_t c,
+                                                  uint32_t rr, int lane, double* s_cand) {
+  return c <= static_cast<uint32_t>(kWave) ? rank_candidates_q<NW, 1>(cand, cw, c, rr, lane, s_cand)
+                                           : rank_candidates_q<NW, 2>(cand, cw, c, rr, lane, s_cand);
 }
 
 // Exact selection for the units the register fast path does not finish (degenerate moments, or a
@@ -664,7 +670,7 @@ __device__ __forceinline__ void select_from_memory(const double* base, int n, in
   if (wave != 0) return;
   const double s_below = sum_partials<NW>(red_tail);
   double s_cand = 0.0;
-  if (!tau_known) tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
+  if (!tau_known) tau = rank_candidates<NW>(cand, wave_counts<NW>(wcount, lane), c, rr, lane, &s_cand);
   const double n_below = static_cast<double>(rank - rr);
   *tau_out = tau;
   *dsum_out = (s_below - n_below * (tau - mu_d)) + s_cand;
@@ -940,6 +946,11 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     uint32_t below = 0;  // all samples below the window
 #pragma unroll
     for (int w = 0; w < NW; ++w) below += wbelow_sh[w];
+    // the bins are wanted only when the target lies in the window (a branch on `below`): without
+    // this the compiler issued their loads inside the branch, a second LDS round trip after the
+    // wait for the counts
+#pragma unroll
+    for (int b = 0; b < NB / kWave; ++b) lds_values_ready(hb[b]);
     if (rank >= below) {
       const ScanResult sr = scan_loaded_bins<NB>(hb, rank - below, lane);  // every wave, same result
       bin = sr.bin;
@@ -992,7 +1003,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     if (lane == 0) wcount[0] = ccount;  // the candidates as one region (wave-local hand-off)
     wave_lds_fence();
     double s_cand;
-    tau = rank_candidates<1>(cand, wcount, c, rr, lane, &s_cand);
+    tau = rank_candidates<1>(cand, wave_counts<1>(wcount, lane), c, rr, lane, &s_cand);
     dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
     DRCVAR_STAMP(6);
   } else if (fast) [[likely]] {
@@ -1017,10 +1028,14 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
     }
-    rch = prm.rc * norm_h(h0, h1);  // R_c |h|: off the histogram's critical path
+    // the per-wave candidate counts are read in the same batch as the tail partials (the ranking
+    // needs them for its candidate addresses; read inside it, they were a second LDS round trip)
+    const uint32_t cw = wave_counts<NW>(wcount, lane);
     const double s_below = sum_partials<NW>(red_tail);
+    lds_values_ready(cw);
+    rch = prm.rc * norm_h(h0, h1);  // R_c |h|: off the histogram's critical path
     double s_cand;
-    tau = rank_candidates<NW>(cand, wcount, c, rr, lane, &s_cand);
+    tau = rank_candidates<NW>(cand, cw, c, rr, lane, &s_cand);
     dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
   } else [[unlikely]] {
     // No spread in the moments: the noise-free step 0 of every obstacle (simulation/obstacles.py:63)
