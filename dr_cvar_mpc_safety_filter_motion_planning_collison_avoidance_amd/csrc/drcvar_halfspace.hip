@@ -46,7 +46,11 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 #ifdef DRCVAR_STAMPS
 // diagnostic build only: per-unit shader-clock stamps at phase boundaries (wave 0)
+#ifdef DRCVAR_STAMPS_WAVES  // + per-wave stamps (slots 8 + 4j + wave) around the load phase
+constexpr int kStampUnits = 16384, kStamps = 16;
+#else
 constexpr int kStampUnits = 16384, kStamps = 8;
+#endif
 __device__ unsigned long long g_stamps[kStampUnits * kStamps];
 #define DRCVAR_STAMP(k)                                                                       \
   do {                                                                                        \
@@ -64,6 +68,18 @@ __device__ unsigned long long g_stamps[kStampUnits * kStamps];
   do {                  \
   } while (0)
 #endif
+#if defined(DRCVAR_STAMPS) && defined(DRCVAR_STAMPS_WAVES)
+#define DRCVAR_STAMP_WAVE(j)                                                                  \
+  do {                                                                                        \
+    const unsigned su_ = blockIdx.y * gridDim.x + blockIdx.x;                                 \
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 256 && su_ < kStampUnits)                    \
+      g_stamps[su_ * kStamps + 8 + 4 * (j) + (threadIdx.x >> 6)] = DRCVAR_STAMP_CLOCK();      \
+  } while (0)
+#else
+#define DRCVAR_STAMP_WAVE(j) \
+  do {                       \
+  } while (0)
+#endif
 
 // Launch-uniform scalars, precomputed on the host so the per-unit critical path carries as few
 // fp64 divisions as possible.
@@ -74,7 +90,7 @@ struct Params {
   double epsilon;
   double eps_over_alpha;  // lambda* epsilon (risk_metrics.py:110,122)
   double inv_n;           // 1 / N
-  double inv_n0;          // 1 / min(N, threads per unit): row-0 subsample for the window
+  double inv_n0;          // 1 / size of the window's subsample (pilot: min(N, 64); row 0: min(N, threads))
   double k;               // alpha N
   double inv_k;           // 1 / (alpha N)
   double z_alpha;         // standard-normal alpha-quantile: centre of the fast-path window
@@ -97,10 +113,13 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // wave primitives: DPP row permutations (each an involution, so every lane of a row ends with the
 // bitwise-identical value), then the four row results combined through readlane in fixed order
 // ---------------------------------------------------------------------------------------------
+// (mov_dpp, not update_dpp with an old value of 0: every lane of these permutations has a source,
+// so the old value is never used, and materialising it cost two v_mov plus a DPP hazard wait per
+// stage of every reduction on the chain)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -239,9 +258,9 @@ __device__ __forceinline__ float mov_dpp_f32(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 template <int CTRL, int KD, int KF>
-__device__ __forceinline__ void sum_stage(double (&v)[KD], float (&f)[KF]) {
-  double td[KD];
-  float tf[KF];
+__device__ __forceinline__ void sum_stage(double* v, float* f) {
+  double td[KD > 0 ? KD : 1];
+  float tf[KF > 0 ? KF : 1];
 #pragma unroll
   for (int q = 0; q < KD; ++q) td[q] = mov_dpp_f64<CTRL>(v[q]);
 #pragma unroll
@@ -251,12 +270,13 @@ __device__ __forceinline__ void sum_stage(double (&v)[KD], float (&f)[KF]) {
 #pragma unroll
   for (int q = 0; q < KF; ++q) f[q] = f[q] + tf[q];
 }
+// (v, f: KD doubles and KF floats in registers — either count may be 0)
 template <int KD, int KF>
-__device__ __forceinline__ void wave_sum_multi(double (&v)[KD], float (&f)[KF]) {
-  sum_stage<kDppQuadXor1>(v, f);
-  sum_stage<kDppQuadXor2>(v, f);
-  sum_stage<kDppHalfMirror>(v, f);
-  sum_stage<kDppMirror>(v, f);
+__device__ __forceinline__ void wave_sum_multi(double* v, float* f) {
+  sum_stage<kDppQuadXor1, KD, KF>(v, f);
+  sum_stage<kDppQuadXor2, KD, KF>(v, f);
+  sum_stage<kDppHalfMirror, KD, KF>(v, f);
+  sum_stage<kDppMirror, KD, KF>(v, f);
 #pragma unroll
   for (int q = 0; q < KD; ++q) v[q] = swap_combine16<OpAdd>(v[q]);
 #pragma unroll
@@ -280,9 +300,9 @@ __device__ __forceinline__ void wave_sum_multi(double (&v)[KD], float (&f)[KF]) 
 // Workgroup sums of the load phase: KD fp64 values (the mean sums) and KF fp32 values (the
 // pivot-shifted second moments, which only position the histogram window).  One barrier.
 template <int NW, int KD, int KF>
-__device__ __forceinline__ void block_sum_moments(double (&v)[KD], float (&f)[KF], double* slot_d,
-                                                  float* slot_f) {
-  wave_sum_multi(v, f);
+__device__ __forceinline__ void block_sum_moments(double* v, float* f, double* slot_d, float* slot_f) {
+  wave_sum_multi<KD, KF>(v, f);
+  DRCVAR_STAMP_WAVE(1);  // diagnostic build: this wave's reduction done, before the barrier
   if constexpr (NW > 1) {
     const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
@@ -768,6 +788,14 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   __shared__ double lane_tail[kList ? BLOCK : 1];
   __shared__ uint32_t wcount[NW];
   __shared__ uint32_t wbelow_sh[NW];
+  // Small plans (the latency-bound ones) place the histogram window from a 64-sample pilot after
+  // barrier 1 — the variance of the projections themselves, one two-value wave reduction —
+  // instead of reducing five row-0 second moments across the workgroup before it: per-wave stamps
+  // (-DDRCVAR_STAMPS_WAVES) showed the seven-value reduction at ~1 000 cycles of one wave's issue
+  // on the chain to barrier 1.  Large plans (bandwidth-bound) keep the row-0 moments, whose larger
+  // subsample gives their narrower windows (0.25 sd at N = 10 000) more margin.
+  constexpr bool kPilot = P <= 8;
+  __shared__ double2 pilot[kPilot ? kWave : 1];
   __shared__ double red_mom[2 * NW];
   __shared__ float red_mom0[5 * NW];
   __shared__ double red_rng[2 * NW];
@@ -823,7 +851,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // round trip in series on the way to the first moment sums.
   const double* dp = dir + o * dir_s_obs + t * dir_s_step;
   const double e0 = dp[0], e1 = dp[1];
-  const double px = base[0], py = base[1];  // pivot (uniform scalar load)
+  const double px = kPilot ? 0.0 : base[0], py = kPilot ? 0.0 : base[1];  // row-0 moments' pivot
   const double inv_n = prm.inv_n, inv_n0 = prm.inv_n0, deg_sq = prm.degenerate_sq;
   const double z_lo = prm.z_lo, hist_scale = prm.hist_scale;
   asm volatile("" ::"s"(e0), "s"(e1), "s"(px), "s"(py), "s"(inv_n), "s"(inv_n0), "s"(deg_sq),
@@ -844,7 +872,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     const double a = valid ? x[j] : 0.0, b = valid ? y[j] : 0.0;
     mom[0] += a;
     mom[1] += b;
-    if (j == 0) {
+    if (!kPilot && j == 0) {
       const float fa = valid ? static_cast<float>(x[0] - px) : 0.f;
       const float fb = valid ? static_cast<float>(y[0] - py) : 0.f;
       mom0[0] = fa;
@@ -854,14 +882,19 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       mom0[4] = fa * fb;
     }
   }
+  if (kPilot && wave == 0) pilot[lane] = make_double2(x[0], y[0]);  // samples 0..63 (lane < n)
   DRCVAR_STAMP(1);
-  block_sum_moments<NW>(mom, mom0, red_mom, red_mom0);                   // [barrier 1]
+  DRCVAR_STAMP_WAVE(0);  // diagnostic build: this wave's samples summed (its loads done)
+  if constexpr (kPilot)
+    block_sum_moments<NW, 2, 0>(mom, mom0, red_mom, red_mom0);           // [barrier 1]
+  else
+    block_sum_moments<NW, 2, 5>(mom, mom0, red_mom, red_mom0);           // [barrier 1]
   DRCVAR_STAMP(2);
   const double mux = mom[0] * inv_n, muy = mom[1] * inv_n;
   // any non-finite sample makes a sum non-finite (so do sums that overflow): solver failure
   const bool bad = !(std::isfinite(mom[0]) && std::isfinite(mom[1]));
 #if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 1
-  if (tid == 0) rec[0] = mux + muy + mom0[0] + mom0[1] + mom0[2] + mom0[3];  // diagnostic
+  if (tid == 0) rec[0] = mux + muy + (kPilot ? 0.f : mom0[0] + mom0[1] + mom0[2] + mom0[3]);
   return;
 #endif
 
@@ -890,10 +923,21 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   for (int j = 0; j < P; ++j)  // +inf padding: never below, inside or a candidate
     d[j] = (tid + j * BLOCK < n) ? project(h0, h1, x[j], y[j]) : INFINITY;
   const double mu_d = h0 * mux + h1 * muy;
-  const double ma0 = mom0[0] * inv_n0, mb0 = mom0[1] * inv_n0;  // row-0 covariance
-  const double cxx = mom0[2] * inv_n0 - ma0 * ma0, cyy = mom0[3] * inv_n0 - mb0 * mb0;
-  const double cxy = mom0[4] * inv_n0 - ma0 * mb0;
-  const double var_d = h0 * h0 * cxx + 2.0 * h0 * h1 * cxy + h1 * h1 * cyy;
+  double var_d;
+  if constexpr (kPilot) {  // variance of the pilot's projections about the exact mean, in fp32
+    const double2 pv = pilot[lane];
+    float fm[2];
+    fm[0] = lane < n ? static_cast<float>(project(h0, h1, pv.x, pv.y) - mu_d) : 0.f;
+    fm[1] = fm[0] * fm[0];
+    wave_sum_multi<0, 2>(nullptr, fm);
+    const double m1 = fm[0] * inv_n0;
+    var_d = fm[1] * inv_n0 - m1 * m1;
+  } else {
+    const double ma0 = mom0[0] * inv_n0, mb0 = mom0[1] * inv_n0;  // row-0 covariance
+    const double cxx = mom0[2] * inv_n0 - ma0 * ma0, cyy = mom0[3] * inv_n0 - mb0 * mb0;
+    const double cxy = mom0[4] * inv_n0 - ma0 * mb0;
+    var_d = h0 * h0 * cxx + 2.0 * h0 * h1 * cxy + h1 * h1 * cyy;
+  }
   // window [wlo, wlo + 2 window_sd sd_d), wlo = mean_d + (z_alpha - window_sd) sd_d; only
   // samples inside it are histogrammed (LDS atomics), samples below it are counted with ballots.
   // Any positive scale keeps the map monotone, so the approximate reciprocal sqrt is exact enough.
@@ -1230,7 +1274,8 @@ void launch_form(const Launch& L) {
 
 template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
 void launch_plan(Launch L, bool vec) {
-  L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < BLOCK ? L.n : BLOCK);
+  const int64_t sub = P <= 8 ? kWave : BLOCK;  // the window's subsample: pilot or row 0 (kernel)
+  L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < sub ? L.n : sub);
   L.prm.hist_scale = static_cast<double>(1 << LOG_NB) / (2.0 * L.prm.window_sd);
   // measured on C5 (2.05 GB): nontemporal 16-B loads 0.746 of HBM peak vs 0.715; on C3 (3.2 MB,
   // cache-resident across steps) they cost 3 %, so only launches larger than the MALL use them

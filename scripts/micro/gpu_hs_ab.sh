@@ -22,3 +22,6 @@ for r in 1 2; do
   one preload scripts/micro/variants/hs_preload.so 20 5 || exit 3
 done
 DRCVAR_DIAG_LIB=scripts/micro/variants/hs_preload.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread 2>&1 | tail -2
+if [ -f scripts/micro/variants/hs_stamps.so ]; then
+  DRCVAR_STAMPS_WAVES=1 DRCVAR_DIAG_LIB=scripts/micro/variants/hs_stamps.so timeout -k 10 120 python3 scripts/stamps.py 2>&1 | grep -v amdgpu.ids
+fi

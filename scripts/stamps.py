@@ -26,10 +26,20 @@ for _ in range(30):
 torch.cuda.synchronize()
 lib = _native.lib()
 U = min(O * T, 16384)
-buf = (ctypes.c_ulonglong * (U * 8))()
+KS = 16 if os.environ.get("DRCVAR_STAMPS_WAVES") else 8  # a -DDRCVAR_STAMPS_WAVES build
+buf = (ctypes.c_ulonglong * (U * KS))()
 lib.drcvar_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 assert lib.drcvar_diag_stamps(ctypes.cast(buf, ctypes.c_void_p), U) == U
-st = np.frombuffer(buf, dtype=np.uint64).reshape(U, 8).astype(np.int64)
+st = np.frombuffer(buf, dtype=np.uint64).reshape(U, KS).astype(np.int64)
+if KS == 16:  # per-wave: loads summed (slots 8..11), reduction done before barrier 1 (12..15)
+    nw = 4
+    ld = st[:, 8:8 + nw] - st[:, :1]
+    rd = st[:, 12:12 + nw] - st[:, :1]
+    print("  per wave, cycles from entry (median over units): loads summed",
+          np.median(ld, 0).round().tolist(), " reduced", np.median(rd, 0).round().tolist(),
+          " barrier 1 passed", float(np.median(st[:, 2] - st[:, 0])))
+    print("  latest wave's loads summed - earliest (median)", float(np.median(ld.max(1) - ld.min(1))))
+    st = st[:, :8]
 names = ["entry->loads done", "moments reduce+barrier1", "h/var/histogram atomics",
          "barrier2+scan", "compaction", "barrier3", "rank+finish"]
 d = np.diff(st, axis=1)
