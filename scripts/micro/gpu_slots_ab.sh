@@ -1,0 +1,27 @@
+#!/usr/bin/env bash
+# C3 A/B of the slot path: the product (slots) against a -DDRCVAR_NO_SLOTS build
+# (scripts/micro/variants/hs_noslots.so), the bench's metric line at K = 2000 and K = 20,
+# interleaved; the GPU suite on the product first; stamps of the slot build last.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/slots_pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/slots_pytest.log; [ $rc -eq 0 ] || exit $rc
+one() {  # one <label> <lib or ""> <steps> <warmup>
+  local lib=$2
+  if [ -n "$lib" ]; then export DRCVAR_DIAG_LIB=$lib; else unset DRCVAR_DIAG_LIB; fi
+  timeout -k 10 200 python3 bench.py --steps $3 --warmup $4 --no-large --no-cpu-baseline 2>&1 | grep "^{" | \
+    python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1 K=$3', round(d['ms_per_step']*1e3,3), round(d['roofline']['kernel_ms']*1e3,3))"
+}
+for r in 1 2 3; do
+  one noslots scripts/micro/variants/hs_noslots.so 2000 200 || exit 3
+  one slots "" 2000 200 || exit 3
+done
+for r in 1 2 3; do
+  one noslots scripts/micro/variants/hs_noslots.so 20 5 || exit 3
+  one slots "" 20 5 || exit 3
+done
+unset DRCVAR_DIAG_LIB
+if [ -f scripts/micro/variants/hs_stamps.so ]; then
+  DRCVAR_DIAG_LIB=scripts/micro/variants/hs_stamps.so timeout -k 10 120 python3 scripts/stamps.py 2>&1 | grep -v amdgpu.ids
+fi
