@@ -299,12 +299,17 @@ __device__ __forceinline__ void wave_sum_multi(double* v, float* f) {
 
 // Workgroup sums of the load phase: KD fp64 values (the mean sums) and KF fp32 values (the
 // pivot-shifted second moments, which only position the histogram window).  One barrier.
-template <int NW, int KD, int KF>
-__device__ __forceinline__ void block_sum_moments(double* v, float* f, double* slot_d, float* slot_f) {
+// `pilot` (optional): the 64-sample pilot published before the barrier — this lane's sample is
+// read in the same batch of LDS reads as the partials (read at its first use, after the direction,
+// it was a second LDS round trip on the chain to the window pass).
+template <int NW, int KD, int KF, bool PILOT = false>
+__device__ __forceinline__ void block_sum_moments(double* v, float* f, double* slot_d, float* slot_f,
+                                                  const double2* pilot = nullptr,
+                                                  double2* pilot_v = nullptr) {
   wave_sum_multi<KD, KF>(v, f);
   DRCVAR_STAMP_WAVE(1);  // diagnostic build: this wave's reduction done, before the barrier
+  const int lane = threadIdx.x & (kWave - 1);
   if constexpr (NW > 1) {
-    const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
     if (lane == 0) {
 #pragma unroll
@@ -313,11 +318,15 @@ __device__ __forceinline__ void block_sum_moments(double* v, float* f, double* s
       for (int q = 0; q < KF; ++q) slot_f[q * NW + w] = f[q];
     }
     __syncthreads();
+    if constexpr (PILOT) *pilot_v = pilot[lane];
 #pragma unroll
     for (int q = 0; q < KD; ++q) v[q] = sum_partials<NW>(slot_d + q * NW);
 #pragma unroll
     for (int q = 0; q < KF; ++q) f[q] = sum_partials<NW>(slot_f + q * NW);
+  } else {
+    if constexpr (PILOT) *pilot_v = pilot[lane];  // (one wave: each lane reads back its own store)
   }
+  if constexpr (PILOT) asm volatile("" ::"v"(pilot_v->x), "v"(pilot_v->y));
 }
 
 // order-preserving map double -> uint64 (total order on non-NaN values)
@@ -854,8 +863,11 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double px = kPilot ? 0.0 : base[0], py = kPilot ? 0.0 : base[1];  // row-0 moments' pivot
   const double inv_n = prm.inv_n, inv_n0 = prm.inv_n0, deg_sq = prm.degenerate_sq;
   const double z_lo = prm.z_lo, hist_scale = prm.hist_scale;
+  // inv_k too: first used by the offsets, it was fetched only after the histogram scan, and the
+  // candidate pass waited for that scalar load (its lgkm wait also covers the kernarg fetch)
+  const double inv_k = prm.inv_k;
   asm volatile("" ::"s"(e0), "s"(e1), "s"(px), "s"(py), "s"(inv_n), "s"(inv_n0), "s"(deg_sq),
-               "s"(z_lo), "s"(hist_scale));
+               "s"(z_lo), "s"(hist_scale), "s"(inv_k), "s"(status));
   // the histogram is cleared while the sample loads are in flight (barrier 1 orders it before
   // the first atomic)
 #pragma unroll
@@ -885,8 +897,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   if (kPilot && wave == 0) pilot[lane] = make_double2(x[0], y[0]);  // samples 0..63 (lane < n)
   DRCVAR_STAMP(1);
   DRCVAR_STAMP_WAVE(0);  // diagnostic build: this wave's samples summed (its loads done)
+  double2 pv = make_double2(0.0, 0.0);  // this lane's pilot sample (small plans)
   if constexpr (kPilot)
-    block_sum_moments<NW, 2, 0>(mom, mom0, red_mom, red_mom0);           // [barrier 1]
+    block_sum_moments<NW, 2, 0, true>(mom, mom0, red_mom, red_mom0, pilot, &pv);  // [barrier 1]
   else
     block_sum_moments<NW, 2, 5>(mom, mom0, red_mom, red_mom0);           // [barrier 1]
   DRCVAR_STAMP(2);
@@ -925,7 +938,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double mu_d = h0 * mux + h1 * muy;
   double var_d;
   if constexpr (kPilot) {  // variance of the pilot's projections about the exact mean, in fp32
-    const double2 pv = pilot[lane];
     float fm[2];
     fm[0] = lane < n ? static_cast<float>(project(h0, h1, pv.x, pv.y) - mu_d) : 0.f;
     fm[1] = fm[0] * fm[0];
