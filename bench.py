@@ -568,7 +568,31 @@ def mpc_handoff(dev, samples, ego, params, with_cpu):
         c5["cpu_oracle_qp_s"] = time.perf_counter() - t0
         c5["max_abs_err_u_vs_oracle"] = float(np.abs(res["u"][0].cpu().numpy() - uo).max())
     out["full_loop_c5"] = c5
-    del ws, rec
+    # ---- main.py's whole flow at C5 size: the halfspaces, then the three safety filters over
+    # them (mean, CVaR, DR-CVaR: main.py:95-112), the three QPs as one launch ----
+    metrics = ("mean", "cvar", "dr_cvar")
+    cols_h = torch.tensor([c for m in metrics for c in (mf.METRIC_COLUMNS[m][0], mf.METRIC_COLUMNS[m][0] + 1)],
+                          device=dev)
+    cols_g = torch.tensor([mf.METRIC_COLUMNS[m][1] for m in metrics], device=dev)
+    x03, xr3, uf3 = x0.expand(3, -1).contiguous(), xr.expand(3, -1, -1).contiguous(), uf.expand(3, -1, -1).contiguous()
+    ws3 = torch.empty(model.workspace_doubles(3, O), dtype=torch.float64, device=dev)
+
+    def three():
+        launch()
+        h3 = rec.index_select(2, cols_h).view(O, T, 3, 2).permute(2, 0, 1, 3)   # [3, O, T, 2]
+        g3 = rec.index_select(2, cols_g).permute(2, 0, 1)                       # [3, O, T]
+        res["info3"] = mf.filter_batch(model, h3, g3, x03, xr3, uf3, workspace=ws3)[2]
+
+    three_ms = timed(three, 5)
+    inf3 = res["info3"].cpu().numpy()
+    out["main_flow_c5"] = {
+        "workload": f"main.py's flow at C5 size: {O} obstacles x {T} steps x {samples.shape[2]} samples -> "
+                    f"halfspaces -> the mean, CVaR and DR-CVaR safety filters (H={H}, {O * T} rows each) "
+                    "as one 3-problem QP launch",
+        "step_ms": three_ms, "qp_workgroups": model.launch_groups(3, O),
+        "qp_status": [mf.STATUS_NAMES.get(int(v)) for v in inf3[:, _native.MPC_INFO_STATUS]],
+        "qp_iterations": [int(v) for v in inf3[:, _native.MPC_INFO_ITERATIONS]]}
+    del ws, ws3, rec
     # ---- batched reference configuration ----
     Hr, Or, Bn = 30, 3, 1024
     model_r = mf.MPCModel(A, Bm, C, Q, R, Hr, ub, pb, device=dev)
