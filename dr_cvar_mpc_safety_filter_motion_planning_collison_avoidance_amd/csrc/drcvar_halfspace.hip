@@ -794,7 +794,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   __shared__ uint32_t hist[hist_words<NB>()];
   __shared__ double cand[NW * kCap];
   __shared__ double win[kList ? NW * P * kWave : 1];
-  __shared__ double lane_tail[kList ? BLOCK : 1];
+  __shared__ double lane_tail[(kList || P <= 8) ? BLOCK : 1];
   __shared__ uint32_t wcount[NW];
   __shared__ uint32_t wbelow_sh[NW];
   // Small plans (the latency-bound ones) place the histogram window from a 64-sample pilot after
@@ -1072,10 +1072,18 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       sq += cj < ubin ? d[j] - mu_d : 0.0;
       append_candidate(cand + wave * kCap, wbase, cj == ubin, d[j], lt_mask);
     }
-    sq = wave_reduce<OpAdd>(sq);
-    if (lane == 0) {
-      red_tail[wave] = sq;
-      wcount[wave] = wbase;
+    if constexpr (kPilot) {
+      // small plans: this lane's tail partial goes to LDS unreduced; wave 0 reduces the four waves'
+      // partials once after barrier 3, beside the ranking's LDS reads, instead of every wave
+      // reducing its own ahead of the barrier
+      lane_tail[tid] = sq;
+      if (lane == 0) wcount[wave] = wbase;
+    } else {
+      sq = wave_reduce<OpAdd>(sq);
+      if (lane == 0) {
+        red_tail[wave] = sq;
+        wcount[wave] = wbase;
+      }
     }
     DRCVAR_STAMP(5);
     __syncthreads();                                                      // [barrier 3]
@@ -1087,8 +1095,20 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     // the per-wave candidate counts are read in the same batch as the tail partials (the ranking
     // needs them for its candidate addresses; read inside it, they were a second LDS round trip)
     const uint32_t cw = wave_counts<NW>(wcount, lane);
-    const double s_below = sum_partials<NW>(red_tail);
-    lds_values_ready(cw);
+    double s_below;
+    if constexpr (kPilot) {
+      double tl[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tl[w] = lane_tail[w * kWave + lane];
+      lds_values_ready(cw);
+      double t = tl[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) t += tl[w];
+      s_below = wave_reduce<OpAdd>(t);
+    } else {
+      s_below = sum_partials<NW>(red_tail);
+      lds_values_ready(cw);
+    }
     rch = prm.rc * norm_h(h0, h1);  // R_c |h|: off the histogram's critical path
     double s_cand;
     tau = rank_candidates<NW>(cand, cw, c, rr, lane, &s_cand);
