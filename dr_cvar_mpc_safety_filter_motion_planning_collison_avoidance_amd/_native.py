@@ -15,15 +15,13 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libdrcvar_halfspace.so")
-# diagnostic builds only (scripts/diag_stages.sh); the product always loads LIB_PATH
-LIB_PATH = os.environ.get("DRCVAR_DIAG_LIB", LIB_PATH)
 SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip"),
            os.path.join(PKG_DIR, "csrc", "drcvar_mpc.hip"),
            os.path.join(PKG_DIR, "csrc", "drcvar_sampling.hip")]
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("drcvar_halfspace.h", "drcvar_mpc.h",
                                                   "drcvar_sampling.h")]
-OFFLOAD_ARCH = os.environ.get("DRCVAR_OFFLOAD_ARCH", "gfx950")
+OFFLOAD_ARCH = "gfx950"  # CDNA4 only
 
 ABI_VERSION = 2
 OUT_WIDTH = 8
@@ -101,6 +99,20 @@ class EngineError(RuntimeError):
 
 _lock = threading.Lock()
 _lib = None
+_lib_path = LIB_PATH  # what lib() loads; only use_library() changes it
+
+
+def use_library(path: str) -> None:
+    """Load ``path`` (a diagnostic variant build, e.g. a stamps build) instead of the product library.
+
+    Diagnostic scripts call this explicitly before the first engine call; nothing in the package
+    reads the environment to pick a library.  Raises if another library is already loaded."""
+    global _lib_path
+    path = os.path.abspath(path)
+    with _lock:
+        if _lib is not None and path != _lib_path:
+            raise NativeLibraryError(f"{_lib_path} is already loaded; use_library({path!r}) must come first")
+        _lib_path = path
 
 
 def _compile_units():
@@ -135,11 +147,14 @@ def build(verbose: bool = False, extra_flags=()) -> str:
     import glob
     incs = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.inc")))  # tables the sources include
     headers = b"".join(open(h, "rb").read() for h in HEADERS + incs)
+    # the compiler's identity is part of every key: objects of an older hipcc / ROCm are rebuilt
+    toolchain = subprocess.run(["hipcc", "--version"], capture_output=True, check=True).stdout
     objs, procs = [], []
     for src, defs in _compile_units():
         flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-I", INCLUDE_DIR,
                  *defs, *extra_flags]
-        key = hashlib.sha256(open(src, "rb").read() + headers + " ".join(flags).encode()).hexdigest()[:16]
+        key = hashlib.sha256(open(src, "rb").read() + headers + toolchain
+                             + " ".join(flags).encode()).hexdigest()[:16]
         tag = "".join(d.replace("-D", ".") for d in defs if d.startswith("-D"))
         obj = os.path.join(obj_dir, f"{os.path.basename(src)}{tag}.{key}.o")
         objs.append(obj)
@@ -160,9 +175,9 @@ def build(verbose: bool = False, extra_flags=()) -> str:
         print(" ".join(link))
     subprocess.run(link, check=True)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    keep = set(objs)  # drop stale cached objects
+    keep = set(objs)  # drop stale cached objects (not *.tmp: another build may be writing them)
     for f in os.listdir(obj_dir):
-        if os.path.join(obj_dir, f) not in keep:
+        if f.endswith(".o") and os.path.join(obj_dir, f) not in keep:
             os.remove(os.path.join(obj_dir, f))
     return LIB_PATH
 
@@ -226,14 +241,14 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
+            if not os.path.exists(_lib_path):
                 raise NativeLibraryError(
-                    f"HIP engine not built: {LIB_PATH} is missing (run __graft_entry__.build() or "
+                    f"HIP engine not built: {_lib_path} is missing (run __graft_entry__.build() or "
                     f"python -m dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.build)")
             try:
-                handle = ctypes.CDLL(LIB_PATH)
+                handle = ctypes.CDLL(_lib_path)
             except OSError as exc:  # pragma: no cover - depends on the ROCm install
-                raise NativeLibraryError(f"cannot load {LIB_PATH}: {exc}") from exc
+                raise NativeLibraryError(f"cannot load {_lib_path}: {exc}") from exc
             _bind(handle)
             if handle.drcvar_abi_version() != ABI_VERSION:
                 raise NativeLibraryError("engine ABI version mismatch; rebuild the library")

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -72,6 +73,8 @@ def make_options(cluster_size=0, spin_limit_us=0, debug_force_resume=False, debu
     o.debug_force_resume = int(bool(debug_force_resume))
     o.debug_perturb_group = 0 if debug_perturb_group is None else int(debug_perturb_group) + 1
     o.debug_perturb_iteration = int(debug_perturb_iteration)
+    if debug_stall_group is not None and int(debug_stall_group) < 1:
+        raise ValueError("debug_stall_group must be >= 1 (workgroup 0 writes the problem's outputs)")
     o.debug_stall_group = 0 if debug_stall_group is None else int(debug_stall_group) + 1
     return o
 
@@ -171,6 +174,35 @@ def filter_batch(model: MPCModel, hs_h: torch.Tensor, hs_g: torch.Tensor, x0: to
     return x, u, info
 
 
+CLUSTER_FAILURES = (_native.MPC_STATUS_CLUSTER_TIMEOUT, _native.MPC_STATUS_CLUSTER_DIVERGED)
+
+
+def retry_cluster_failures(model: MPCModel, hs_h, hs_g, x0, x_ref, u_fallback, x, u, info,
+                           max_iter: int = DEFAULT_MAX_ITER, tol: float = DEFAULT_TOL,
+                           polish: bool = True, stream=None):
+    """Re-solve, on one workgroup each, the problems of a :func:`filter_batch` result that ended
+    CLUSTER_TIMEOUT or CLUSTER_DIVERGED (a cluster whose workgroups could not all stay resident, or
+    disagreed), so that the caller gets the optimum the reference would return rather than the
+    fallback rollout.  Synchronises (reads the status column); patches x / u / info in place and
+    warns once per call that retried.  Returns the indices retried."""
+    status = info[:, _native.MPC_INFO_STATUS].cpu()
+    bad = torch.nonzero((status == CLUSTER_FAILURES[0]) | (status == CLUSTER_FAILURES[1])).flatten()
+    if bad.numel() == 0:
+        return []
+    warnings.warn(f"{bad.numel()} clustered QP solve(s) ended "
+                  f"{sorted({STATUS_NAMES.get(int(status[i])) for i in bad})}; re-solving them on one "
+                  "workgroup each", RuntimeWarning, stacklevel=2)
+    idx = bad.to(x.device)
+    pick = lambda t: t.index_select(0, idx)
+    x1, u1, info1 = filter_batch(model, pick(hs_h), pick(hs_g), pick(x0), pick(x_ref),
+                                 pick(u_fallback), max_iter, tol, polish, stream=stream,
+                                 options=make_options(cluster_size=1))
+    x.index_copy_(0, idx, x1)
+    u.index_copy_(0, idx, u1)
+    info.index_copy_(0, idx, info1)
+    return bad.tolist()
+
+
 def record_views(record: torch.Tensor, metric: str):
     """(h [1, O, T, 2], g [1, O, T]) views of an ``[O, T, 8]`` halfspace record for ``metric``."""
     ch, cg = METRIC_COLUMNS[metric]
@@ -263,6 +295,7 @@ class MPCSafetyFilter:
         xr_d = torch.as_tensor(_host(x_ref)[None, :H + 1]).to(dev)
         uf_d = torch.as_tensor(self._fallback_inputs(u_ref)[None]).to(dev)
         x, u, info = filter_batch(m, hs_h, hs_g, x0_d, xr_d, uf_d, self.max_iter, self.tol)
+        retry_cluster_failures(m, hs_h, hs_g, x0_d, xr_d, uf_d, x, u, info, self.max_iter, self.tol)
         x, u, info = x[0].cpu().numpy(), u[0].cpu().numpy(), info[0].cpu().numpy()
         status = STATUS_NAMES.get(int(info[_native.MPC_INFO_STATUS]), "error")
         if status in SOLVED:                                       # :154-167

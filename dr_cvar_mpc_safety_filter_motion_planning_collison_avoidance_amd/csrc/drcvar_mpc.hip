@@ -2888,6 +2888,9 @@ int drcvar_mpc_filter_f64_ex(const drcvar_mpc_model* model, const double* blob, 
   drcvar_mpc_options opt{};
   if (options) opt = *options;
   if (opt.cluster_size < 0 || opt.spin_limit_us < 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  // workgroup 0 of a cluster writes the problem's outputs after the final exchange: stalling it
+  // would leave them unwritten instead of reporting CLUSTER_TIMEOUT, so the hook names groups >= 1
+  if (opt.debug_stall_group == 1 || opt.debug_stall_group < 0) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (n_problems == 0) return DRCVAR_OK;
   if (!x0 || !x_ref || !u_fallback || !x_out || !u_out || !info_out) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (max_iter < 1 || !(tol > 0.0) || n_problems > 0x7fffffffLL) return DRCVAR_ERR_INVALID_ARGUMENT;

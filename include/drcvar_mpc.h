@@ -79,8 +79,9 @@ extern "C" {
  *     debug_perturb_group       g + 1: workgroup g of every cluster scales its step length by
  *                               (1 - 2^-20) at interior-point iteration debug_perturb_iteration
  *                               (must end with DRCVAR_MPC_STATUS_CLUSTER_DIVERGED)
- *     debug_stall_group         g + 1: workgroup g of every cluster leaves before the final
- *                               exchange (must end with DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT)
+ *     debug_stall_group         g + 1: workgroup g (g >= 1) of every cluster leaves before the
+ *                               final exchange (must end with DRCVAR_MPC_STATUS_CLUSTER_TIMEOUT);
+ *                               g = 0 is rejected (workgroup 0 writes the outputs)
  */
 typedef struct drcvar_mpc_options {
   int32_t cluster_size;

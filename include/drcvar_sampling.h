@@ -16,7 +16,12 @@
  *
  * Random numbers: Philox4x32-10 (counter-based; key = seed, counter = (unit * ceil(N/2) + pair,
  * stream)), one call per PAIR of samples of a unit -> two (32-bit uniform, 32-bit turn) pairs ->
- * Box-Muller -> z ~ N(0, I2); sample = nominal + L z with L the lower Cholesky factor of noise_cov.  Same distribution as the reference's
+ * Box-Muller -> z ~ N(0, I2); sample = nominal + L z with L the lower Cholesky factor of noise_cov.
+ * Tail: the radius uniform is 32-bit (u = (2x + 1) 2^-33 >= 2^-33), so |z| <= sqrt(66 ln 2) = 6.76
+ * and the far tail is quantised in steps of 2^-32 in u; the reference's 53-bit draws exceed 6.76 sd
+ * with probability 2^-33 per sample (~0.0075 samples per 128 M-sample C5 refill).  Below the cap the
+ * Rayleigh tail frequencies are kept (tests/test_sampling.py::test_device_sampler_radius_tail).
+ * Same distribution as the reference's
  * np.random.multivariate_normal, not the same stream (numpy's MT19937 is sequential; the host
  * mirror in simulation/obstacles.py reproduces that stream exactly).  Output is a pure function
  * of (seed, stream_offset, indices): deterministic and independent of the launch geometry.

@@ -4,6 +4,9 @@ many-problem form (one launch of 150) and the few-problem form (launches of <= 1
 records, and the oracle distance of the first few.  GPU only; honours DRCVAR_DIAG_LIB."""
 import sys, os
 sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import diaglib  # noqa: E402
+diaglib.apply()  # DRCVAR_DIAG_LIB: a variant build (diagnostics)
 import numpy as np, torch
 import test_mpc as tm
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf

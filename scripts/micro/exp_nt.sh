@@ -9,6 +9,6 @@ for v in base nt; do
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -I include $F $SRC -o /tmp/exp_$v.so || exit 1
 done
 for w in c5 c3 c5 c3; do for v in base nt; do
-  DRCVAR_DIAG_LIB=/tmp/exp_$v.so timeout -k 10 200 python bench.py --workload $w --steps 200 --warmup 10 --graph-batch 10 --no-large --no-cpu-baseline --no-mpc > gpurun_out/exp_${v}_$w.log 2>&1 || exit 2
+  timeout -k 10 200 python bench.py --lib /tmp/exp_$v.so --workload $w --steps 200 --warmup 10 --graph-batch 10 --no-large --no-cpu-baseline --no-mpc > gpurun_out/exp_${v}_$w.log 2>&1 || exit 2
   python3 -c "import json,sys; r=json.loads(open('gpurun_out/exp_${v}_$w.log').read().strip().splitlines()[-1]); print('$v $w', r['value'], r['roofline']['frac'], r['roofline']['kernel_ms'])"
 done; done

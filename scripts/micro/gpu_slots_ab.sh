@@ -10,7 +10,7 @@ rc=$?; tail -3 gpurun_out/slots_pytest.log; [ $rc -eq 0 ] || exit $rc
 one() {  # one <label> <lib or ""> <steps> <warmup>
   local lib=$2
   if [ -n "$lib" ]; then export DRCVAR_DIAG_LIB=$lib; else unset DRCVAR_DIAG_LIB; fi
-  timeout -k 10 200 python3 bench.py --steps $3 --warmup $4 --no-large --no-cpu-baseline 2>&1 | grep "^{" | \
+  timeout -k 10 200 python3 bench.py ${DRCVAR_DIAG_LIB:+--lib $DRCVAR_DIAG_LIB} --steps $3 --warmup $4 --no-large --no-cpu-baseline 2>&1 | grep "^{" | \
     python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1 K=$3', round(d['ms_per_step']*1e3,3), round(d['roofline']['kernel_ms']*1e3,3))"
 }
 for r in 1 2 3; do

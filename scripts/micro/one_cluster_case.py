@@ -5,6 +5,9 @@ import sys
 
 sys.path.insert(0, os.getcwd())
 sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import diaglib  # noqa: E402
+diaglib.apply()  # DRCVAR_DIAG_LIB: a variant build (diagnostics)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

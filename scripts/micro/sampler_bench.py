@@ -6,6 +6,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import diaglib  # noqa: E402
+diaglib.apply()  # DRCVAR_DIAG_LIB: a variant build (diagnostics)
 
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.simulation import obstacles
 

@@ -4,6 +4,9 @@ buffer, then the sampler refill with the product library and with DRCVAR_DIAG_LI
 import ctypes, os, subprocess, sys
 import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import diaglib  # noqa: E402
+diaglib.apply()  # DRCVAR_DIAG_LIB: a variant build (diagnostics)
 dev = torch.device("cuda", 0)
 out = torch.empty((256, 50, 10000, 2), dtype=torch.float64, device=dev)
 src = torch.empty_like(out)

@@ -16,6 +16,11 @@ OFFSET_TOL = 1e-6
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    # A/B runs of the suite against a variant build (scripts/micro/*.sh): the test harness, not the
+    # package, chooses the library
+    if os.environ.get("DRCVAR_DIAG_LIB"):
+        from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
+        _native.use_library(os.environ["DRCVAR_DIAG_LIB"])
 
 
 def golden_files():

@@ -82,3 +82,55 @@ def test_shard_pieces_rejects_bad_blocks():
         sharding.shard_pieces(2, 3, 4, 7)
     assert sharding.shard_pieces(2, 3, 2, 2) == []
     assert sharding.shard_pieces(4, 5, 3, 17) == [(0, 1, 3, 5, 0), (1, 3, 0, 5, 2), (3, 4, 0, 2, 12)]
+
+
+def test_cluster_failure_retry_path(monkeypatch):
+    """problems that end CLUSTER_TIMEOUT / CLUSTER_DIVERGED are re-solved on one
+    workgroup each (options.cluster_size = 1) and patched into the batch result, with a warning."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    B, O, H, nx, nu = 4, 3, 5, 4, 2
+    hs_h, hs_g = torch.zeros(B, O, H, 2, dtype=torch.float64), torch.zeros(B, O, H, dtype=torch.float64)
+    x0, xr, uf = torch.zeros(B, nx, dtype=torch.float64), torch.zeros(B, H + 1, nx, dtype=torch.float64), \
+        torch.zeros(B, H, nu, dtype=torch.float64)
+    x = torch.zeros(B, H + 1, nx, dtype=torch.float64)
+    u = torch.zeros(B, H, nu, dtype=torch.float64)
+    info = torch.zeros(B, _native.MPC_INFO_WIDTH, dtype=torch.float64)
+    info[1, 0] = _native.MPC_STATUS_CLUSTER_TIMEOUT
+    info[3, 0] = _native.MPC_STATUS_CLUSTER_DIVERGED
+    info[2, 0] = _native.MPC_STATUS_NUMERICAL          # not a cluster failure: left alone
+    calls = []
+
+    def fake(model, h, g, x0_, xr_, uf_, max_iter, tol, polish, stream=None, options=None):
+        calls.append((h.shape[0], options.cluster_size))
+        n = h.shape[0]
+        inf = torch.zeros(n, _native.MPC_INFO_WIDTH, dtype=torch.float64)
+        inf[:, 1] = 7
+        return (torch.full((n, H + 1, nx), 1.0, dtype=torch.float64),
+                torch.full((n, H, nu), 2.0, dtype=torch.float64), inf)
+
+    monkeypatch.setattr(mf, "filter_batch", fake)
+    with pytest.warns(RuntimeWarning, match="re-solving"):
+        got = mf.retry_cluster_failures(None, hs_h, hs_g, x0, xr, uf, x, u, info)
+    assert got == [1, 3] and calls == [(2, 1)]
+    assert torch.all(u[[1, 3]] == 2.0) and torch.all(u[[0, 2]] == 0.0)
+    assert info[1, 0] == 0 and info[3, 1] == 7 and info[2, 0] == _native.MPC_STATUS_NUMERICAL
+    calls.clear()
+    assert mf.retry_cluster_failures(None, hs_h, hs_g, x0, xr, uf, x, u, info) == [] and calls == []
+
+
+def test_stall_hook_rejects_output_group():
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    with pytest.raises(ValueError):
+        mf.make_options(debug_stall_group=0)
+    assert mf.make_options(debug_stall_group=2).debug_stall_group == 3
+
+
+def test_product_loader_reads_no_environment():
+    """The library path is fixed unless use_library() is called (VERDICT r3 hygiene): the loader's
+    source reads no environment variable."""
+    import inspect
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
+    src = inspect.getsource(_native)
+    assert "os.environ" not in src and "getenv" not in src
+    assert _native.LIB_PATH.endswith("_lib/libdrcvar_halfspace.so")

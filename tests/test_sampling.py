@@ -150,6 +150,24 @@ def test_device_sampler_moments_and_normality(dev):
 
 
 @pytest.mark.gpu
+def test_device_sampler_radius_tail(dev):
+    """the Box-Muller radius comes from a 32-bit uniform (u >= 2^-33), so |z| is capped
+    at sqrt(66 ln 2) = 6.76 sd (P(R > 6.76) = 2^-33 for the reference's 53-bit draws: 0.0075 samples
+    per 128 M-sample C5 refill).  The tail below the cap must keep the Rayleigh frequencies
+    P(R > r) = exp(-r^2 / 2): counts of R > 3, 4, 5 sd over 32 M samples within 5 Poisson sd."""
+    import torch
+    nom = torch.zeros((1, 2, 2), dtype=torch.float64, device=dev)
+    N = 1 << 25
+    s = ob.sample_trajectories_device(nom, N, np.eye(2), seed=2024)[0, 1]
+    r2 = (s * s).sum(-1)
+    assert float(r2.max()) <= 66 * np.log(2) + 1e-9
+    for r in (3.0, 4.0, 5.0):
+        got = int((r2 > r * r).sum())
+        want = N * np.exp(-r * r / 2)
+        assert abs(got - want) < 5 * np.sqrt(want) + 1, (r, got, want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("O,T,N,seed,stream,zero_first", [(2, 3, 5000, 123, 0, True),
                                                           (3, 5, 777, 2 ** 40 + 9, 2 ** 33 + 1, False),
                                                           (1, 2, 1, 0, 0, True)])
