@@ -157,9 +157,11 @@ class Stepper:
                 torch.cuda.synchronize(dev)
 
     def _one(self, launch=None):
-        if self.compute:
+        if self.compute and self.exchange:
+            self.sb.step(launch)          # kernel + all-gather (pipelined by chunks when chunks > 1)
+        elif self.compute:
             self.sb.compute(launch)
-        if self.exchange:
+        elif self.exchange:
             self.sb.exchange()
 
     def _capture(self, n):
@@ -243,6 +245,8 @@ def main():
     ap.add_argument("--strong-workloads", default="c4,c5",
                     help="global batches of the strong-scaling legs (sharded over the ranks), comma-separated")
     ap.add_argument("--strong-steps", type=int, default=20)
+    ap.add_argument("--chunks", type=int, default=2,
+                    help="strong-scaling legs at N > 1: also time the pipelined step with this many chunks")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -409,6 +413,20 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload)
            "phases_rank_max": {"kernel_ms": kernel_s * 1e3, "allgather_ms": gather_ms,
                                "timing": f"HIP events over {K} steps of the phase alone, max over ranks"},
            "kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK}
+    if world > 1 and args.chunks > 1:
+        # the pipelined step (sharding.chunked_all_gather): the rank's block in `chunks` launches,
+        # chunk j's all-gather issued behind chunk j + 1's kernel; same records, same order
+        sbc = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed, gather_device=gdev,
+                                    chunks=args.chunks)
+        stc = Stepper(sbc, mode, 10, K, dev)
+        stc.run(min(K, 10))
+        el_c, _, _ = timed(world, lambda: stc.run(K), dev, stream)
+        same = bool(torch.equal(sbc.records().to(sb.records().device), sb.records()))
+        step_c = el_c / K * 1e3
+        out["pipelined"] = {"chunks": args.chunks, "value": sb.U * K / el_c, "ms_per_step": step_c,
+                            "overlap_ms": kernel_s * 1e3 + gather_ms - step_c,
+                            "records_equal_unpipelined": same, "launch": stc.describe()}
+        del stc, sbc
     # full loop: + the QP hand-off on every rank (core/mpc_filter.py:116-151 takes all halfspaces)
     if workload == "c5" and not args.no_mpc:
         import numpy as np

@@ -59,7 +59,7 @@
 namespace drcvar_mpc_detail {
 
 struct BlobLayout {
-  int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, total;
+  int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, UF1, UF2, UFOK, total;
 };
 
 inline BlobLayout blob_layout(int nx, int nu, int H) {
@@ -76,6 +76,11 @@ inline BlobLayout blob_layout(int nx, int nu, int H) {
   L.C = o; o += 2 * nx;
   L.Q = o; o += nx * nx;
   L.R = o; o += nu * nu;
+  // the tracking optimum without rows, u_free = -H0^-1 f = UF1 x0 + UF2 xr (the starting point):
+  // UF1 = -H0^-1 F1 [n x nx], UF2 = H0^-1 F2 [n x H*nx]; UFOK = 1 when H0 factored (else u = 0)
+  L.UF1 = o; o += n * nx;
+  L.UF2 = o; o += n * H * nx;
+  L.UFOK = o; o += 1;
   L.total = o;
   return L;
 }
@@ -148,6 +153,11 @@ constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
 constexpr double kPolishDualTol = 1e-7;
 constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
+constexpr double kStartMuMany = 20.0;   // barrier parameter of the starting point, >= 64 obstacles
+constexpr double kStartMuFew = 1.0;     // ... fewer obstacles
+constexpr double kStartDualCap = 0.5 * kSlackLin;  // largest starting lambda_hs
+constexpr double kStartBoxMargin = 0.05;  // starting inputs at least this fraction of the box inside
+constexpr double kStartFloorW = 1e-2;     // smallest starting slack of a bound row
 constexpr int kResumeIters = 8;         // interior-point iterations after a failed polish
 constexpr double kResumeTol = 1e-3;     // ... towards tol * kResumeTol
 constexpr double kPolishEqTol = 1e-12;  // multiplier passes stop at |E u - e| <= this * (1 + max|g|)
@@ -459,6 +469,24 @@ __device__ __forceinline__ double rcp(double x) {
 // step-to-boundary ratio; only feeds the 0.995 fraction of the step length, so the raw estimate
 __device__ __forceinline__ double ratio(double x, double dx) {
   return dx < 0.0 ? -x * __builtin_amdgcn_rcp(dx) : kHuge;
+}
+
+// Central-path slack of a halfspace row with residual r at barrier parameter mu: the root s >
+// max(r, 0) of g(s) = (50 + 100 s)(s - r) s - mu (2 s - r), i.e. 50 + 100 s = mu / (s - r) + mu / s.
+// g is convex and increasing beyond max(r, 0) (g'' = 600 s + 100 - 200 r > 0 there) and
+// g(max(r, 0)) <= 0, so Newton's method from a point where g > 0 (s0 = max(r, 0) + 1 + mu / 50, for
+// mu <= 75) decreases monotonically to the root and never leaves (max(r, 0), s0].
+__device__ inline double start_slack(double r, double mu) {
+  double sv = fmax(r, 0.0) + 1.0 + mu * (1.0 / kSlackLin);
+  for (int i = 0; i < 60; ++i) {
+    const double a = kSlackLin + kSlackHess * sv, b = sv - r;
+    const double gv = a * b * sv - mu * (2.0 * sv - r);
+    const double gd = kSlackHess * b * sv + a * (2.0 * sv - r) - 2.0 * mu;
+    const double step = gv / gd;
+    sv -= step;
+    if (!(step > 1e-14 * sv)) break;  // converged (or not finite: stop)
+  }
+  return sv;
 }
 
 // p[2k+i] = c[2k+i] + sum_{j<=k} Mp[k-j][i][:] . u[j*nu : (j+1)*nu].  The sum over j is split
@@ -1642,21 +1670,44 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     for (int t = 0; t < H; ++t)
       for (int q = 0; q < nx; ++q) acc -= f2[t * nx + q] * xr[(t + 1) * a.xr_st + q];
     s.f[j] = acc;
-    s.u[j] = 0.0;
+    // starting inputs: the tracking optimum without rows, u = -H0^-1 f (UF1 x0 + UF2 xr, condensed
+    // on the host), strictly inside the input box
+    double u0 = 0.0;
+    if (a.blob[a.off.UFOK] != 0.0) {
+      const double* g1 = a.blob + a.off.UF1 + static_cast<int64_t>(j) * nx;
+      const double* g2 = a.blob + a.off.UF2 + static_cast<int64_t>(j) * H * nx;
+      for (int q = 0; q < nx; ++q) u0 += g1[q] * x0[q];
+      for (int t = 0; t < H; ++t)
+        for (int q = 0; q < nx; ++q) u0 += g2[t * nx + q] * xr[(t + 1) * a.xr_st + q];
+    }
+    if (a.has_u) {
+      const int ai = j % NU;
+      const double span = a.umax[ai] - a.umin[ai];
+      u0 = fmin(fmax(u0, a.umin[ai] + kStartBoxMargin * span), a.umax[ai] - kStartBoxMargin * span);
+    }
+    s.u[j] = u0;
   }
   __syncthreads();
+  positions<NU, kBlock>(s, s.u, s.p, s.c, H);
+  __syncthreads();
 
-  // start: u = 0, s = 0, w = max(d - Gz, 1), lambda = 1 except the slack rows' (below).  With
-  // many obstacles the halfspace rows start at lambda = 5 and their slack rows at w = 1.5: counted
-  // on the CPU restatement (scripts/micro/ipm_lab.py) over three families of device-dumped
-  // problems (72 in all: scripts/mpc_bench.py's, a wider seed set of them, and bench.py's C5-style
-  // hand-offs) that is 7 % fewer iterations in each family and 6-13 % on the 256-obstacle ones;
-  // with a few obstacles (main.py: 3) the unit start stays ahead, so the switch is by obstacle count.
+  // Start (round 4): every inequality on the central path of barrier parameter mu0 at the starting
+  // inputs u (above).  A halfspace row with residual r = h.p + g takes the slack s > max(r, 0) that
+  // minimises 50 s + 50 s^2 - mu0 log(s - r) - mu0 log(s) (start_slack), so that w_hs = s - r,
+  // w_s = s, lambda = mu0 / w and the row's own stationarity 50 + 100 s = lambda_hs + lambda_s hold,
+  // except that lambda_hs is capped at 25 (a row violated at u would start with lambda_hs ~ 50 +
+  // 100 r: main.py's mean-metric filter at C5 size then took 20-23 iterations instead of 16-17);
+  // the bound rows take lambda = mu0 / w.  Counted on the CPU restatement (scripts/micro/ipm_lab.py
+  // --start central_mu=20,central_mu_few=1,u_free=1,many=64,lam_cap=25 on the problem sets of
+  // scripts/micro/make_qp_set.py) against the round-3 start (u = 0, unit or (5, 1.5) duals):
+  // bench-like DR-CVaR C5 problems 78 -> 64 iterations over six seeds (the degenerate C5 fixture
+  // 14 -> 10), main.py's three filters at C5 size and H = 20 / 10 obstacles 180 -> 151 (C5 mean
+  // 50 -> 50, C5 CVaR 42 -> 33), main.py-like problems with 3-10 obstacles 106 -> 76.
   const bool many_rows = O >= kManyRowsObstacles;
-  const double lA0 = many_rows ? 5.0 : 1.0, wB0 = many_rows ? 1.5 : 1.0;
+  const double mu0 = many_rows ? kStartMuMany : kStartMuFew;
   double gmax = 0.0;
   if (lane < K) {
-    const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
+    const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
     for (int o = o_lo + wave; o < o_hi; o += kWaves) {
       const double* hp = a.hs_h + b * a.h_sp + o * a.h_so + lane * a.h_sk;
       const double g = a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk];
@@ -1665,34 +1716,36 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       rows.h0[r] = h0;
       rows.h1[r] = h1;
       rows.g[r] = g;
-      rows.s[r] = 0.0;
-      rows.wA[r] = fmax(-(h0 * c0 + h1 * c1 + g), 1.0);
-      rows.lA[r] = lA0;
-      rows.wB[r] = wB0;
-      // the dual of s >= 0 ends at kSlackLin - lambda_hs in [0, kSlackLin] (kSlackLin where the
-      // halfspace is slack, the common case): start midway, not at 1 (main.py QP 9 -> 6
-      // iterations, C5 18 -> 16; 10, 25 and 50 measured, 25 best across the shapes)
-      rows.lB[r] = 0.5 * kSlackLin;
+      const double res = h0 * p0 + h1 * p1 + g;
+      const double sv = start_slack(res, mu0);
+      const double wA = sv - res;
+      rows.s[r] = sv;
+      rows.wA[r] = wA;
+      rows.lA[r] = fmin(mu0 * rcp(wA), kStartDualCap);
+      rows.wB[r] = sv;
+      rows.lB[r] = mu0 * rcp(sv);
       gmax = fmax(gmax, fabs(g));
     }
   }
   if (a.has_u) {
     for (int j = tid; j < n; j += kBlock) {
       const int ai = j % NU;
-      s.bx[j] = fmax(a.umax[ai], 1.0);
-      s.bx[n + j] = 1.0;
-      s.bx[2 * n + j] = fmax(-a.umin[ai], 1.0);
-      s.bx[3 * n + j] = 1.0;
+      const double wu = fmax(a.umax[ai] - s.u[j], kStartFloorW), wl = fmax(s.u[j] - a.umin[ai], kStartFloorW);
+      s.bx[j] = wu;
+      s.bx[n + j] = mu0 / wu;
+      s.bx[2 * n + j] = wl;
+      s.bx[3 * n + j] = mu0 / wl;
       gmax = fmax(gmax, fmax(fabs(a.umin[ai]), fabs(a.umax[ai])));
     }
   }
   if (a.has_p) {
     for (int t = tid; t < 2 * H; t += kBlock) {
       const int i = t & 1;
-      s.px[t] = fmax(a.pmax[i] - s.c[t], 1.0);
-      s.px[2 * H + t] = 1.0;
-      s.px[4 * H + t] = fmax(s.c[t] - a.pmin[i], 1.0);
-      s.px[6 * H + t] = 1.0;
+      const double wu = fmax(a.pmax[i] - s.p[t], kStartFloorW), wl = fmax(s.p[t] - a.pmin[i], kStartFloorW);
+      s.px[t] = wu;
+      s.px[2 * H + t] = mu0 / wu;
+      s.px[4 * H + t] = wl;
+      s.px[6 * H + t] = mu0 / wl;
       gmax = fmax(gmax, fmax(fabs(a.pmin[i]), fabs(a.pmax[i])));
     }
   }
@@ -2838,6 +2891,48 @@ int drcvar_mpc_model_init(const double* A, const double* B, const double* C, con
         blob[L.CA + (p * 2 + i) * nx + j] = acc;
       }
     }
+  // UF1 = -H0^-1 F1, UF2 = H0^-1 F2 by a Cholesky factorisation of H0 (SPD when R is; otherwise
+  // UFOK = 0 and the kernel starts from u = 0)
+  {
+    std::vector<double> Lc(static_cast<size_t>(n) * n, 0.0);
+    bool ok = true;
+    for (int j = 0; j < n && ok; ++j) {
+      double d = H0[j * n + j];
+      for (int k = 0; k < j; ++k) d -= Lc[j * n + k] * Lc[j * n + k];
+      if (!(d > 0.0) || !std::isfinite(d)) { ok = false; break; }
+      const double ljj = std::sqrt(d);
+      Lc[j * n + j] = ljj;
+      for (int i = j + 1; i < n; ++i) {
+        double acc = H0[i * n + j];
+        for (int k = 0; k < j; ++k) acc -= Lc[i * n + k] * Lc[j * n + k];
+        Lc[i * n + j] = acc / ljj;
+      }
+    }
+    const int ncols = nx + H * nx;  // right-hand sides: the columns of F1, then of F2
+    std::vector<double> col(n);
+    for (int c = 0; c < ncols; ++c) {
+      for (int r = 0; r < n; ++r)
+        col[r] = c < nx ? -F1[r * nx + c] : F2[static_cast<size_t>(r) * H * nx + (c - nx)];
+      if (ok) {
+        for (int r = 0; r < n; ++r) {  // L y = col
+          double acc = col[r];
+          for (int k = 0; k < r; ++k) acc -= Lc[r * n + k] * col[k];
+          col[r] = acc / Lc[r * n + r];
+        }
+        for (int r = n - 1; r >= 0; --r) {  // L' x = y
+          double acc = col[r];
+          for (int k = r + 1; k < n; ++k) acc -= Lc[k * n + r] * col[k];
+          col[r] = acc / Lc[r * n + r];
+        }
+      }
+      for (int r = 0; r < n; ++r) {
+        const double v = ok ? col[r] : 0.0;
+        if (c < nx) blob[L.UF1 + r * nx + c] = v;
+        else blob[L.UF2 + static_cast<int64_t>(r) * H * nx + (c - nx)] = v;
+      }
+    }
+    blob[L.UFOK] = ok ? 1.0 : 0.0;
+  }
   std::memcpy(blob + L.A, A, sizeof(double) * nx * nx);
   std::memcpy(blob + L.B, B, sizeof(double) * nx * nu);
   std::memcpy(blob + L.C, C, sizeof(double) * 2 * nx);

@@ -34,14 +34,54 @@ from . import engine
 from .engine import RiskParams
 
 
-def shard_bounds(n_units: int, world_size: int, rank: int) -> tuple[int, int]:
-    """Contiguous block ``[start, stop)`` of rank ``rank`` (blocks of ceil(U/W); the tail rank may
-    get fewer or zero units)."""
-    if world_size < 1 or not (0 <= rank < world_size):
-        raise ValueError("invalid rank/world_size")
+def block_units(n_units: int, world_size: int, align: int = 1) -> int:
+    """Units per rank block: ceil(U/W), rounded up to a multiple of ``align`` (the chunk count of a
+    pipelined exchange, so every chunk of every block has the same length)."""
     per = -(-n_units // world_size) if n_units else 0
+    return -(-per // align) * align
+
+
+def shard_bounds(n_units: int, world_size: int, rank: int, align: int = 1) -> tuple[int, int]:
+    """Contiguous block ``[start, stop)`` of rank ``rank`` (blocks of :func:`block_units`; the tail
+    rank may get fewer or zero units)."""
+    if world_size < 1 or not (0 <= rank < world_size) or align < 1:
+        raise ValueError("invalid rank/world_size/align")
+    per = block_units(n_units, world_size, align)
     start = min(rank * per, n_units)
     return start, min(start + per, n_units)
+
+
+def chunked_all_gather(full: torch.Tensor, send: torch.Tensor, chunks: int, compute_chunk=None,
+                       scratch: torch.Tensor | None = None, group=None) -> None:
+    """The records exchange, pipelined behind the kernel: ``send [per, 8]`` (``per = chunks *
+    cs``) is produced chunk by chunk (``compute_chunk(j)`` fills ``send[j cs:(j + 1) cs]``); each
+    chunk's all-gather is issued asynchronously as soon as its kernel is queued (RCCL: on the
+    communicator's stream, ordered after that kernel by an event), so chunk j's collective runs
+    while chunk j + 1's kernel does.  The gathered chunks land in ``scratch [chunks, W cs, 8]``
+    (chunk-major) and one copy puts them into ``full [W per, 8]`` in rank-major order — the same
+    bytes, in the same ``[O, T, 8]`` order, as one all-gather of the whole block.
+    ``chunks == 1``: compute, then one ``all_gather_into_tensor(full, send)``."""
+    world = dist.get_world_size(group)
+    per, width = send.shape
+    if chunks == 1:
+        if compute_chunk is not None:
+            compute_chunk(0)
+        _all_gather(full, send, group)
+        return
+    cs = per // chunks
+    if cs * chunks != per or scratch is None or tuple(scratch.shape) != (chunks, world * cs, width):
+        raise ValueError("chunked exchange: send must hold chunks * cs rows and scratch [chunks, W cs, 8]")
+    works = []
+    for j in range(chunks):
+        if compute_chunk is not None:
+            compute_chunk(j)
+        src = send[j * cs:(j + 1) * cs]
+        if src.device != scratch.device:             # gloo rehearsal: device records via the host
+            src = src.to(scratch.device)
+        works.append(dist.all_gather_into_tensor(scratch[j], src, group=group, async_op=True))
+    for w in works:
+        w.wait()
+    full.view(world, chunks, cs, width).copy_(scratch.view(chunks, world, cs, width).transpose(0, 1))
 
 
 def shard_pieces(n_obstacles: int, n_steps: int, start: int, stop: int):
@@ -100,20 +140,35 @@ def gather_records(send: torch.Tensor, n_units: int, group=None) -> torch.Tensor
 
 
 def sharded_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: RiskParams,
-                            group=None, gather: bool = True, compute=engine_compute):
+                            group=None, gather: bool = True, compute=engine_compute, chunks: int = 1):
     """Evaluate this rank's share of an ``[O, T, N, 2]`` batch; with ``gather`` return the full
-    ``[O, T, 8]`` record on every rank, else ``(local [u, 8], start, stop)``."""
+    ``[O, T, 8]`` record on every rank, else ``(local [u, 8], start, stop)``.  ``chunks > 1``: the
+    block is evaluated in that many pieces, each all-gathered while the next is computed
+    (:func:`chunked_all_gather`; identical records)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     O, T = samples.shape[:2]
-    views, start, stop = shard_views(samples, ego, world, rank)
-    per = -(-(O * T) // world) if O * T else 0
+    start, stop = shard_bounds(O * T, world, rank, align=chunks)
+    per = block_units(O * T, world, chunks)
     send = torch.zeros((per, engine.OUT_WIDTH), dtype=torch.float64, device=samples.device)
-    for s, e, off, cnt in views:
-        compute(s, e, params, send[off:off + cnt].view(s.shape[0], s.shape[1], engine.OUT_WIDTH))
+    cs = per // chunks if per else 0
+
+    def compute_chunk(j):
+        a, b = min(start + j * cs, stop), min(start + (j + 1) * cs, stop)
+        for o0, o1, t0, t1, off in shard_pieces(O, T, a, b):
+            cnt = (o1 - o0) * (t1 - t0)
+            dst = send[a - start + off:a - start + off + cnt]
+            compute(samples[o0:o1, t0:t1], ego[t0:t1], params, dst.view(o1 - o0, t1 - t0, engine.OUT_WIDTH))
+
     if not gather:
+        for j in range(chunks):
+            compute_chunk(j)
         return send[:stop - start], start, stop
-    return gather_records(send, O * T, group).reshape(O, T, engine.OUT_WIDTH)
+    full = torch.empty((per * world, engine.OUT_WIDTH), dtype=torch.float64, device=samples.device)
+    scratch = (torch.empty((chunks, world * cs, engine.OUT_WIDTH), dtype=torch.float64, device=samples.device)
+               if chunks > 1 else None)
+    chunked_all_gather(full, send, chunks, compute_chunk, scratch, group)
+    return full[:O * T].reshape(O, T, engine.OUT_WIDTH)
 
 
 class ShardedBatch:
@@ -131,7 +186,7 @@ class ShardedBatch:
     def __init__(self, nominal: torch.Tensor, ego: torch.Tensor, n_samples: int, params: RiskParams,
                  world_size: int = 1, rank: int = 0, group=None, seed: int = 42,
                  stream_offset: int = 0, noise_cov=None, zero_first_step: bool = True,
-                 gather_device=None):
+                 gather_device=None, chunks: int = 1, force_exchange: bool = False):
         from .simulation import obstacles
         O, T = int(nominal.shape[0]), int(nominal.shape[1])
         dev = nominal.device
@@ -139,9 +194,11 @@ class ShardedBatch:
         self.U = O * T
         self.world, self.rank, self.group = world_size, rank, group
         self.params, self.nominal, self.seed = params, nominal, seed
-        self.start, self.stop = shard_bounds(self.U, world_size, rank)
+        self.chunks = int(chunks)
+        self.start, self.stop = shard_bounds(self.U, world_size, rank, align=self.chunks)
         self.count = self.stop - self.start
-        self.per = -(-self.U // world_size) if self.U else 0
+        self.per = block_units(self.U, world_size, self.chunks)
+        self.cs = self.per // self.chunks if self.per else 0
         cov = obstacles.NOISE_COV if noise_cov is None else noise_cov
         self.samples = obstacles.sample_units_device(nominal, self.N, self.start, self.count, cov,
                                                      seed=seed, stream_offset=stream_offset,
@@ -150,34 +207,54 @@ class ShardedBatch:
         self.ego_units = ego.index_select(0, idx).contiguous()            # [count, 2], built once
         self.send = torch.zeros((self.per, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
         gdev = dev if gather_device is None else torch.device(gather_device)
+        # force_exchange: the collective runs at world 1 too (tests / the 1-rank RCCL rehearsal)
+        exchange = world_size > 1 or force_exchange
         self.full = (torch.empty((self.per * world_size, engine.OUT_WIDTH), dtype=torch.float64,
-                                 device=gdev) if world_size > 1 else None)
+                                 device=gdev) if exchange else None)
+        self.scratch = (torch.empty((self.chunks, world_size * self.cs, engine.OUT_WIDTH),
+                                    dtype=torch.float64, device=gdev)
+                        if exchange and self.chunks > 1 else None)
         self._launch = self.prepare()
 
     def prepare(self, stream=None):
-        """A frozen launch of this rank's block on ``stream`` (default: the current stream) — for
-        hipGraph capture pass the capturing stream."""
-        if self.count == 0:
-            return None
-        launch, _ = engine.prepare_safe_halfspaces(
-            self.samples.unsqueeze(0), self.ego_units, self.params,
-            out=self.send[:self.count].view(1, self.count, engine.OUT_WIDTH), stream=stream)
-        return launch
+        """Frozen launches of this rank's block on ``stream`` (default: the current stream), one
+        per chunk — for hipGraph capture pass the capturing stream."""
+        launches = []
+        for j in range(self.chunks):
+            a, b = min(j * self.cs, self.count), min((j + 1) * self.cs, self.count)
+            if a == b:
+                launches.append(None)
+                continue
+            launch, _ = engine.prepare_safe_halfspaces(
+                self.samples[a:b].unsqueeze(0), self.ego_units[a:b], self.params,
+                out=self.send[a:b].view(1, b - a, engine.OUT_WIDTH), stream=stream)
+            launches.append(launch)
+        return launches
+
+    def _compute_chunk(self, launches, j) -> None:
+        if launches[j] is not None:
+            launches[j]()
 
     def compute(self, launch=None) -> None:
         """The halfspace kernel over this rank's units (no collective)."""
-        launch = launch if launch is not None else self._launch
-        if launch is not None:
-            launch()
+        launches = launch if launch is not None else self._launch
+        for j in range(self.chunks):
+            self._compute_chunk(launches, j)
 
     def exchange(self) -> None:
         """The QP hand-off exchange: every rank's records to every rank (no-op at world 1)."""
         if self.full is not None:
-            _all_gather(self.full, self.send, self.group)
+            chunked_all_gather(self.full, self.send, self.chunks, None, self.scratch, self.group)
 
     def step(self, launch=None) -> None:
-        self.compute(launch)
-        self.exchange()
+        """One step: the kernel and the exchange — with ``chunks > 1`` pipelined, chunk j's
+        all-gather behind chunk j + 1's kernel (:func:`chunked_all_gather`)."""
+        launches = launch if launch is not None else self._launch
+        if self.full is None:
+            self.compute(launches)
+            return
+        chunked_all_gather(self.full, self.send, self.chunks,
+                           lambda j: self._compute_chunk(launches, j), self.scratch, self.group)
 
     def local_records(self) -> torch.Tensor:
         """``[count, 8]`` records of this rank's units (a view of the all-gather input)."""

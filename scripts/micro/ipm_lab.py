@@ -71,6 +71,28 @@ def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False, 
     wUl, lUl = np.maximum(-md["umin"], 1.0), np.full(n, bl)
     wPu, lPu = np.maximum(md["pmax"] - c, 1.0), np.full(2 * H, bl)
     wPl, lPl = np.maximum(c - md["pmin"], 1.0), np.full(2 * H, bl)
+    if START.get("u_free", 0.0) > 0.0:       # the tracking optimum without rows, clipped to the box
+        span = md["umax"] - md["umin"]
+        u = np.clip(-np.linalg.solve(md["H0"], f), md["umin"] + 0.05 * span, md["umax"] - 0.05 * span)
+        pu = c + Gp @ u
+        wUu, wUl = md["umax"] - u, u - md["umin"]
+        wPu, wPl = np.maximum(md["pmax"] - pu, START.get("wp_floor", 1e-2)), np.maximum(pu - md["pmin"], START.get("wp_floor", 1e-2))
+    if START.get("central_mu", 0.0) > 0.0:   # every row on its own central path at u
+        cmu = START["central_mu"] if O >= START.get("many", 1e9) else START.get("central_mu_few", START["central_mu"])
+        r = hp_of(c + Gp @ u) + g
+        lo, hi = np.maximum(r, 0.0), np.maximum(r, 0.0) + 1.0 + 2.0 * np.sqrt(cmu)
+        for _ in range(200):
+            mid = 0.5 * (lo + hi)
+            phi = SLACK_LIN + SLACK_HESS * mid - cmu / (mid - r) - cmu / mid
+            lo, hi = np.where(phi < 0, mid, lo), np.where(phi < 0, hi, mid)
+        s = 0.5 * (lo + hi)
+        wA, wB = s - r, s.copy()
+        lA, lB = cmu / wA, cmu / wB
+        if START.get("lam_cap", 0.0) > 0.0:
+            lA = np.minimum(lA, START["lam_cap"])
+        bmu = START.get("central_box_mu", cmu)
+        lUu, lUl = bmu / wUu, bmu / wUl
+        lPu, lPl = bmu / wPu, bmu / wPl
     scale_d = 1.0 + max(np.abs(g).max(), 5.0, 10.0)
     scale_q = 1.0 + max(np.abs(f).max(), SLACK_LIN)
     m = 2 * O * H + 2 * n + 4 * H

@@ -20,11 +20,45 @@ from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core impor
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.engine import RiskParams  # noqa: E402
 
 
+_HIP = None
+_RAW_STREAMS = []  # (HIP handle, raw stream) created here, destroyed by destroy_streams()
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        import ctypes
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    return _HIP
+
+
+def _masked_stream(dev, words, what):
+    """A raw HIP stream with the CU mask `words`, wrapped for torch.  The raw stream is recorded so
+    that destroy_streams() can synchronise and destroy it through the same HIP handle before the
+    process exits: left alive, its queue was torn down by the runtime's static destructors after the
+    profiler had finalised, and the process died in __cxa_finalize (pipe_prof.log)."""
+    import ctypes
+    hip = _hip()
+    mask = (ctypes.c_uint32 * len(words))(*words)
+    h = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), mask)
+    assert rc == 0, f"hipExtStreamCreateWithCUMask: {rc}"
+    _RAW_STREAMS.append(h)
+    print(f"CU-masked halfspace stream: {what}", flush=True)
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def destroy_streams():
+    hip = _hip() if _RAW_STREAMS else None
+    while _RAW_STREAMS:
+        h = _RAW_STREAMS.pop()
+        assert hip.hipStreamSynchronize(h) == 0
+        assert hip.hipStreamDestroy(h) == 0
+
+
 def cu_masked_stream(dev, reserve):
     """A HIP stream whose kernels may use every CU but `reserve` of them (every (n/reserve)-th bit of
     the CU mask cleared, so the reserved CUs spread over the XCDs whatever the bit order)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
     n = torch.cuda.get_device_properties(dev).multi_processor_count
     words = [0xFFFFFFFF] * ((n + 31) // 32)
     if n % 32:
@@ -33,30 +67,18 @@ def cu_masked_stream(dev, reserve):
     for k in range(reserve):
         b = k * step
         words[b // 32] &= ~(1 << (b % 32))
-    mask = (ctypes.c_uint32 * len(words))(*words)
-    h = ctypes.c_void_p()
-    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), mask)
-    assert rc == 0, f"hipExtStreamCreateWithCUMask: {rc}"
-    print(f"CU-masked halfspace stream: {n} CUs, {reserve} reserved", flush=True)
-    return torch.cuda.ExternalStream(h.value, device=dev)
+    return _masked_stream(dev, words, f"{n} CUs, {reserve} reserved")
 
 
 def cu_allowed_stream(dev, allow):
     """A HIP stream whose kernels may use only `allow` CUs (every (n/allow)-th bit of the mask)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
     n = torch.cuda.get_device_properties(dev).multi_processor_count
     words = [0] * ((n + 31) // 32)
     step = n // allow
     for k in range(allow):
         b = k * step
         words[b // 32] |= 1 << (b % 32)
-    mask = (ctypes.c_uint32 * len(words))(*words)
-    h = ctypes.c_void_p()
-    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), mask)
-    assert rc == 0, f"hipExtStreamCreateWithCUMask: {rc}"
-    print(f"CU-masked halfspace stream: {allow} of {n} CUs", flush=True)
-    return torch.cuda.ExternalStream(h.value, device=dev)
+    return _masked_stream(dev, words, f"{allow} of {n} CUs")
 
 
 def main():
@@ -136,6 +158,9 @@ def main():
     print("QP status seq/pipe", mf.STATUS_NAMES.get(int(i_seq[0, 0])), mf.STATUS_NAMES.get(int(i_pipe[0, 0])),
           "iterations", int(i_seq[0, 1]), int(i_pipe[0, 1]),
           "u bitwise equal", bool(np.array_equal(u_seq, u_pipe)), "max|du|", float(np.abs(u_seq - u_pipe).max()))
+    del hs_s, pipe_launch, res
+    destroy_streams()
+    print("streams destroyed", flush=True)
 
 
 if __name__ == "__main__":

@@ -76,6 +76,7 @@ def main():
               f"{B / ms * 1e3:.0f} QPs/s, "
               f"iters {inf[:, _native.MPC_INFO_ITERATIONS].mean():.1f}, "
               f"polished {inf[:, _native.MPC_INFO_POLISHED].mean():.2f}, "
+              f"polish attempts {inf[:, _native.MPC_INFO_POLISH_ATTEMPTS].mean():.2f}, "
               f"optimal {(st == 0).mean():.2f}, fallback {inf[:, _native.MPC_INFO_USED_FALLBACK].mean():.2f}",
               flush=True)
 

@@ -166,7 +166,16 @@ def test_model_init_condensation(dyn):
         o += size
     tail = np.concatenate([A.ravel(), B.ravel(), C.ravel(), Q.ravel(), R.ravel()])
     np.testing.assert_array_equal(blob[o:o + tail.size], tail)
-    assert o + tail.size == m.blob_doubles
+    o += tail.size
+    # the starting point's maps: u_free = -H0^-1 f = UF1 x0 + UF2 xr, then the flag
+    uf1 = -np.linalg.solve(ref["H0"], ref["F1"])
+    uf2 = np.linalg.solve(ref["H0"], ref["F2"])
+    for name, want in (("UF1", uf1), ("UF2", uf2)):
+        np.testing.assert_allclose(blob[o:o + want.size], want.reshape(-1), rtol=1e-9,
+                                   atol=1e-8 * np.abs(want).max(), err_msg=name)
+        o += want.size
+    assert blob[o] == 1.0
+    assert o + 1 == m.blob_doubles
 
 
 def test_model_init_bounds_and_validation():

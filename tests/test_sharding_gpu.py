@@ -109,8 +109,9 @@ def test_rccl_world1_sharded_batch_step_eager_and_graph(dev, rccl_group):
     eagerly and inside a captured hipGraph (launch + all_gather_into_tensor per step)."""
     O, T, N = 8, 10, 1000
     nominal, ego = _nominal(O, T, dev, seed=9)
-    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, group=rccl_group, seed=9)
-    sb.full = torch.full((sb.per, 8), float("nan"), dtype=torch.float64, device=dev)  # force the collective
+    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, group=rccl_group, seed=9,
+                               force_exchange=True)
+    sb.full.fill_(float("nan"))
     sb.step()
     torch.cuda.synchronize()
     whole_s, _ = synthetic.obstacle_batch(O, T, N, dev, seed=9)
@@ -128,17 +129,20 @@ def test_rccl_world1_sharded_batch_step_eager_and_graph(dev, rccl_group):
     assert torch.equal(sb.records(), want)
 
 
-def test_rccl_world1_c4_leg_phases(dev, rccl_group):
+@pytest.mark.parametrize("chunks", [1, 2, 3])
+def test_rccl_world1_c4_leg_phases(dev, rccl_group, chunks):
     """bench.py's C4 strong-scaling leg (BASELINE config 4: 64 obstacles x T 30 x N 5000, the
     RCCL all-gather config) on a 1-rank RCCL group with the collective forced on: the stepper of
     the whole step, of the kernel alone and of the all-gather alone (the phase splits the leg
-    reports), graph-captured; the gathered records equal the single-launch evaluation of the
-    same batch, and the C oracle on a strided subset of units."""
+    reports), graph-captured; with chunks > 1 the step is the pipelined form (chunk j's
+    all-gather issued behind chunk j + 1's kernel).  The gathered records equal the single-launch
+    evaluation of the same batch, and the C oracle on a strided subset of units."""
     import bench
     O, T, N = bench.WORKLOADS["c4"][:3]
     nominal, ego = _nominal(O, T, dev, seed=11)
-    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, group=rccl_group, seed=11)
-    sb.full = torch.full((sb.per, 8), float("nan"), dtype=torch.float64, device=dev)  # force the collective
+    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, group=rccl_group, seed=11,
+                               chunks=chunks, force_exchange=True)
+    sb.full.fill_(float("nan"))
     whole_s, _ = synthetic.obstacle_batch(O, T, N, dev, seed=11)
     want = engine.safe_halfspaces(whole_s, ego, RiskParams())
     for kw in ({}, {"exchange": False}, {"compute": False}):
