@@ -41,7 +41,13 @@ constexpr int kCap = 128;          // candidates ranked directly (per-wave regio
 constexpr int kMaxValueIters = 3;  // value-linear refinements before switching to integer keys
 constexpr double kSentinel = 100.0;
 constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2;  // sample load forms (kernel template)
-constexpr int64_t kNtBytes = 256ll << 20;  // launches reading more than the MALL use kLoadNt
+#ifndef DRCVAR_NT_BYTES  // diagnostic builds may move the threshold (scripts/micro A/B runs)
+#define DRCVAR_NT_BYTES (256ll << 20)
+#endif
+constexpr int64_t kNtBytes = DRCVAR_NT_BYTES;  // launches reading more than the MALL use kLoadNt
+#ifndef DRCVAR_HS_LDS_PAD  // diagnostic builds: extra dynamic LDS per workgroup (caps residency)
+#define DRCVAR_HS_LDS_PAD 0
+#endif
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 #ifdef DRCVAR_STAMPS
@@ -1296,7 +1302,7 @@ void launch_form(const Launch& L) {
     const int64_t chunk = n_obs - o0 < kMaxGridY ? n_obs - o0 : kMaxGridY;
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
                        dim3(static_cast<unsigned>(L.n_steps), static_cast<unsigned>(chunk)),
-                       dim3(BLOCK), 0, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
+                       dim3(BLOCK), DRCVAR_HS_LDS_PAD, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
                        static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
                        L.dir + o0 * L.dir_s_obs, L.dir_s_obs, L.dir_s_step, L.prm,
                        L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH,

@@ -1659,6 +1659,13 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     for (int q = 0; q < nx; ++q) acc += ca[q] * x0[q];
     s.c[t] = acc;
   }
+  // x_ref[1..H] staged in LDS (s.xs, the output rollout's buffer, is free until then): every
+  // thread of the two sums below reads all of it
+  for (int e = tid; e < H * nx; e += kBlock) {
+    const int t = e / nx, q = e - t * nx;
+    s.xs[e] = xr[(t + 1) * a.xr_st + q];
+  }
+  __syncthreads();
   // f = F1 x0 - F2 xr, summed in this order on purpose: splitting the sum (as the Gp'z sums are)
   // moved the rounding of f enough to stall one degenerate test problem (generic1, H = 64) at
   // merit 1e-8 with a failing polish (degenerate active sets defeat the polish)
@@ -1668,17 +1675,32 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     double acc = 0.0;
     for (int q = 0; q < nx; ++q) acc += f1[q] * x0[q];
     for (int t = 0; t < H; ++t)
-      for (int q = 0; q < nx; ++q) acc -= f2[t * nx + q] * xr[(t + 1) * a.xr_st + q];
+      for (int q = 0; q < nx; ++q) acc -= f2[t * nx + q] * s.xs[t * nx + q];
     s.f[j] = acc;
-    // starting inputs: the tracking optimum without rows, u = -H0^-1 f (UF1 x0 + UF2 xr, condensed
-    // on the host), strictly inside the input box
-    double u0 = 0.0;
-    if (a.blob[a.off.UFOK] != 0.0) {
-      const double* g1 = a.blob + a.off.UF1 + static_cast<int64_t>(j) * nx;
+  }
+  // starting inputs: the tracking optimum without rows, u = -H0^-1 f = UF1 x0 + UF2 xr (condensed
+  // on the host), strictly inside the input box; the UF2 x_ref sums as interleaved partial sums
+  // (threads (j, part)), so no thread carries a chain of H nx loads
+  constexpr int kParts = kBlock >= 512 ? 4 : 2;
+  const bool have_uf = a.blob[a.off.UFOK] != 0.0;
+  if (have_uf) {
+    for (int e = tid; e < n * kParts; e += kBlock) {
+      const int j = e / kParts, part = e - (e / kParts) * kParts;
       const double* g2 = a.blob + a.off.UF2 + static_cast<int64_t>(j) * H * nx;
+      double acc = 0.0;
+      for (int t = part; t < H; t += kParts)
+        for (int q = 0; q < nx; ++q) acc += g2[t * nx + q] * s.xs[t * nx + q];
+      s.red[e] = acc;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += kBlock) {
+    double u0 = 0.0;
+    if (have_uf) {
+      const double* g1 = a.blob + a.off.UF1 + static_cast<int64_t>(j) * nx;
       for (int q = 0; q < nx; ++q) u0 += g1[q] * x0[q];
-      for (int t = 0; t < H; ++t)
-        for (int q = 0; q < nx; ++q) u0 += g2[t * nx + q] * xr[(t + 1) * a.xr_st + q];
+#pragma unroll
+      for (int part = 0; part < kParts; ++part) u0 += s.red[j * kParts + part];
     }
     if (a.has_u) {
       const int ai = j % NU;

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# Round 4: the MPC kernel with the central-path start — GPU MPC tests, then scripts/mpc_bench.py and
-# bench.py's hand-off legs against the round-3 library (scripts/micro/variants/mpc_r3.so), interleaved.
+# Round 4 MPC A/B: GPU MPC tests on the product, then scripts/mpc_bench.py and bench.py's hand-off
+# legs for the product against variants (scripts/micro/variants/<name>.so; VARIANTS="r3 start").
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
@@ -9,15 +9,13 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   tests/test_mpc.py tests/test_mpc_cluster.py > $OUT/tests.log 2>&1; rc=$?
 tail -15 $OUT/tests.log
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit 2
-for r in 1; do
-  for v in new r3; do
-    lib=""; [ $v = r3 ] && lib=scripts/micro/variants/mpc_r3.so
-    echo "== mpc_bench $v"
-    DRCVAR_DIAG_LIB=$lib timeout -k 10 300 python3 -u scripts/mpc_bench.py --shapes 30,3,1 30,3,1024 20,10,3 50,256,1 50,256,3 2>&1 | grep -v amdgpu.ids || exit 3
-  done
+for v in product ${VARIANTS:-}; do
+  lib=""; [ $v != product ] && lib=scripts/micro/variants/mpc_$v.so
+  echo "== mpc_bench $v"
+  DRCVAR_DIAG_LIB=$lib timeout -k 10 300 python3 -u scripts/mpc_bench.py --shapes 30,3,1 30,3,1024 20,10,3 50,256,1 50,256,3 2>&1 | grep -v amdgpu.ids || exit 3
 done
-for v in new r3; do
-  lib=""; [ $v = r3 ] && lib=scripts/micro/variants/mpc_r3.so
+for v in product ${VARIANTS:-}; do
+  lib=""; [ $v != product ] && lib=scripts/micro/variants/mpc_$v.so
   timeout -k 10 400 python3 bench.py ${lib:+--lib $lib} --steps 200 --warmup 20 --no-cpu-baseline > $OUT/bench_$v.json 2>$OUT/bench_$v.err || exit 4
   python3 - $OUT/bench_$v.json $v <<'PY'
 import json, sys

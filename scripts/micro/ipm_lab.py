@@ -253,7 +253,7 @@ def main():
         START[k] = float(v)
     z = np.load(args.npz)
     keys = sorted({k.rsplit("_", 1)[0] for k in z.files if k.endswith("_h")})
-    tot_k, tot_l, c5 = 0, 0, 0
+    tot_k, tot_l, c5, its = 0, 0, 0, []
     for key in keys:
         if args.only and args.only not in key:
             continue
@@ -266,12 +266,14 @@ def main():
             err = np.abs(u.reshape(-1) - ub[b].reshape(-1)).max()
             tot_k += kit
             tot_l += it
+            its.append(it)
             if "O256" in key:
                 c5 += it
             if not args.quiet:
                 print(f"{key} b{b}: lab {it:2d} iterations (kernel {kit:2d}), |u - u_kernel| {err:.1e}",
                   flush=True)
-    print(f"{args.variant} {args.start}: total iterations: lab {tot_l} (C5 {c5}), kernel {tot_k}")
+    print(f"{args.variant} {args.start}: total iterations: lab {tot_l} (C5 {c5}), kernel {tot_k}, "
+          f"max {max(its)}, histogram {np.bincount(its).tolist()}")
 
 
 if __name__ == "__main__":

@@ -17,6 +17,8 @@ from oracle import closed_form  # noqa: E402
 SHAPES = [(50, 256, s) for s in range(6)] + [(30, 64, s) for s in range(3)] + [(20, 100, s) for s in range(3)]
 if os.environ.get("QP_SET") == "metrics":  # main.py's three filters at C5 size
     SHAPES = [(50, 256, s, m) for s in range(3) for m in ("mean", "cvar")] + [(20, 10, s, m) for s in range(4) for m in ("mean", "cvar", "dr")]
+if os.environ.get("QP_SET") == "batch":  # mpc_bench.py's 30,3,B shape: many seeds
+    SHAPES = [(30, 3, s) for s in range(64)]
 if os.environ.get("QP_SET") == "small":  # main.py-like: a few obstacles, H = 30 / 20
     SHAPES = [(30, 3, s) for s in range(8)] + [(20, 10, s) for s in range(4)] + [(40, 6, s) for s in range(4)]
 
@@ -51,7 +53,7 @@ def main():
                     f"{key}_u": np.zeros((1, H, 2)), f"{key}_info": np.zeros((1, 10))})
         print(key, flush=True)
     os.makedirs(os.path.join(REPO, "scripts", "micro", "data"), exist_ok=True)
-    np.savez_compressed(os.path.join(REPO, "scripts", "micro", "data", {"small": "qp_small.npz", "metrics": "qp_metrics.npz"}.get(os.environ.get("QP_SET"), "qp_set.npz")), **out)
+    np.savez_compressed(os.path.join(REPO, "scripts", "micro", "data", {"small": "qp_small.npz", "metrics": "qp_metrics.npz", "batch": "qp_batch.npz"}.get(os.environ.get("QP_SET"), "qp_set.npz")), **out)
 
 
 if __name__ == "__main__":

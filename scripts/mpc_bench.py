@@ -74,7 +74,9 @@ def main():
         st = inf[:, _native.MPC_INFO_STATUS]
         print(f"H={H} O={O} B={B} groups={model.launch_groups(B, O, opt)}: {ms:.3f} ms/launch, "
               f"{B / ms * 1e3:.0f} QPs/s, "
-              f"iters {inf[:, _native.MPC_INFO_ITERATIONS].mean():.1f}, "
+              f"iters {inf[:, _native.MPC_INFO_ITERATIONS].mean():.1f} (max {inf[:, _native.MPC_INFO_ITERATIONS].max():.0f}, "
+              f"hist {np.bincount(inf[:, _native.MPC_INFO_ITERATIONS].astype(int)).tolist()}), "
+              f"max polish attempts {inf[:, _native.MPC_INFO_POLISH_ATTEMPTS].max():.0f}, "
               f"polished {inf[:, _native.MPC_INFO_POLISHED].mean():.2f}, "
               f"polish attempts {inf[:, _native.MPC_INFO_POLISH_ATTEMPTS].mean():.2f}, "
               f"optimal {(st == 0).mean():.2f}, fallback {inf[:, _native.MPC_INFO_USED_FALLBACK].mean():.2f}",
