@@ -551,6 +551,31 @@ __device__ inline void gpt_parts(const Lds& s, const double* z, const double* H0
     part_sum[e] = acc;
   }
 }
+// One thread's (Gp' z)[j_a] (+ (H0 u)[j_a] with H0), summed exactly as gpt_parts + parts_total do
+// it (the PARTS interleaved partial sums, combined in order): the same bits from one thread, for
+// the waves that form the affine rhs beside the factorisation
+template <int NU, int kBlock>
+__device__ inline double gpt_row(const Lds& s, const double* z, const double* H0, const double* u,
+                                 int j_a, int n, int H) {
+  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
+  const int j = j_a / NU, a = j_a - (j_a / NU) * NU;
+  double tot = 0.0;
+#pragma unroll
+  for (int part = 0; part < PARTS; ++part) {
+    double acc = 0.0;
+    for (int k = j + part; k < H; k += PARTS) {
+      const double* m = s.Mp + (k - j) * 2 * NU;
+      acc += m[a] * z[2 * k] + m[NU + a] * z[2 * k + 1];
+    }
+    if (H0) {
+      const double* h0r = H0 + static_cast<int64_t>(j_a) * n;
+      for (int l = part; l < n; l += PARTS) acc += h0r[l] * u[l];
+    }
+    tot = part == 0 ? acc : tot + acc;
+  }
+  return tot;
+}
+
 template <int kBlock>
 __device__ __forceinline__ double parts_total(const double* part_sum, int j) {
   constexpr int PARTS = kBlock >= 512 ? 4 : 2;
@@ -637,164 +662,22 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[N
   return ok;
 }
 
-// Factorisation for NX = 4 (the reference's double integrator and every smaller model) with the
-// recursion's state in registers: lane (i, j) of a 16-lane row holds P_{k+1}[i][j], and a step
-// moves data between lanes only through the cross-lane paths of the register file — DPP quad
-// broadcasts for a row of a matrix (lane (i, m) -> every lane of quad i) and ds_swizzle bit-mask
-// patterns for a column (lane (m, j) -> every lane of column j: the LDS crossbar, no LDS memory,
-// no fence) — instead of the two LDS hand-offs per step of the entry-by-entry form below:
-//   T = P A (lane (i, j)), U = P B (row i, every lane of it); columns of T and all of U by swizzle
-//   Re = Rb + B'U, its inverse (every lane, identical operands in canonical order: uniform)
-//   L[:, i] = U'A[:, i], L[:, j] = U'A[:, j] (the same formula for both columns, so mirrored lanes
-//   see the same values), Kg[:, j] = Re^-1 L[:, j]
-//   P_k = Qb_k + (A'T)[i][j] - L[:, i]' Re^-1 L[:, j]
-// Qb and L'Re^-1 L are evaluated in a form whose rounding is symmetric in (i, j) (no fma
-// contraction, commutative products and pair sums); A'PA is not, so P_k is mirrored from its
-// lower triangle by one ds_bpermute (the recursion must stay exactly symmetric, see above).
-// Every row of wave 0 computes the same (rows 1..3 replicate row 0; only row 0 stores).
-// MEASURED AND NOT KEPT (round 3; build with -DDRCVAR_MPC_RICCATI_REGS): C5 QP 0.948 -> 1.033 ms,
-// main.py's 1024-problem batch 0.559 -> 0.751 ms, and the generic3 H = 40 test 8.5e-6 off the
-// oracle.  ds_swizzle and ds_bpermute go through the LDS unit like the reads they replace (two
-// hand-offs per step either way), there are 26 of them per step, and computing L from U = PB
-// instead of from T = PA decorrelates the rounding of the two huge terms whose difference is P.
-template <int M>
-__device__ __forceinline__ double qrow_f64(double v) {  // lane (i, M) of quad i, to the quad
-  constexpr int ctrl = M | (M << 2) | (M << 4) | (M << 6);
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-template <int M>
-__device__ __forceinline__ double qcol_f64(double v) {  // lane (M, j) of the row of 16, to lane (*, j)
-  constexpr int pattern = 0x3 | ((M << 2) << 5);      // bit-mask mode: (lane & 3) | (M << 2)
-  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pattern);
-  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pattern);
-  return __hiloint2double(hi, lo);
-}
+// (Round 3 measured a register form of the NX = 4 step — P in registers, rows and columns moved by
+// DPP quad broadcasts and ds_swizzle, ~26 cross-lane moves per step — and did not keep it: C5 QP
+// 0.948 -> 1.033 ms)
 
-template <int NU>
-__device__ inline bool riccati_factor_regs4(const Lds& s, int H) {
-#pragma clang fp contract(off)
-  const int lane = threadIdx.x & 63;
-  const int e = lane & 15, i = e >> 2, j = e & 3;
-  const int tr_addr = 4 * ((lane & ~15) | (j * 4 + i));  // the transposed entry's lane
-  double Aj[4], Ai[4], Bm[4][NU], R2[NU][NU];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    Aj[m] = s.Am[m * kMx + j];
-    Ai[m] = s.Am[m * kMx + i];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) Bm[m][c] = s.Bm[m * NU + c];
-  }
-#pragma unroll
-  for (int c = 0; c < NU; ++c)
-#pragma unroll
-    for (int d = 0; d < NU; ++d) R2[c][d] = 2.0 * s.Rm[c * NU + d];
-  const double c0i = s.Cm[i], c1i = s.Cm[kMx + i], c0j = s.Cm[j], c1j = s.Cm[kMx + j];
-  const double q2 = s.Qm[i * kMx + j] + s.Qm[j * kMx + i];  // 2Q for a symmetric Q, symmetric always
-  const double cc00 = c0i * c0j, cc11 = c1i * c1j, cc01 = c0i * c1j + c1i * c0j;
-  auto qb = [&](int k) {  // Qb_{k+1} = 2Q + C'S_k C, entry (i, j), symmetric rounding
-    const double S00 = s.S[k], S01 = s.S[H + k], S11 = s.S[2 * H + k];
-    return q2 + ((S00 * cc00 + S11 * cc11) + S01 * cc01);
-  };
-  double p = qb(H - 1);
-  bool ok = true;
-  for (int k = H - 1; k >= 0 && ok; --k) {
-    double du[NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) du[c] = s.DU[k * NU + c];
-    const double qnext = k > 0 ? qb(k - 1) : 0.0;
-    // row i of P
-    const double r0 = qrow_f64<0>(p), r1 = qrow_f64<1>(p), r2 = qrow_f64<2>(p), r3 = qrow_f64<3>(p);
-    // T[i][j] = P[i,:] A[:, j], U[i][c] = P[i,:] B[:, c]
-    const double t = (r0 * Aj[0] + r1 * Aj[1]) + (r2 * Aj[2] + r3 * Aj[3]);
-    double u[NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) u[c] = (r0 * Bm[0][c] + r1 * Bm[1][c]) + (r2 * Bm[2][c] + r3 * Bm[3][c]);
-    // column j of T, all of U (canonical row order m = 0..3)
-    const double tc[4] = {qcol_f64<0>(t), qcol_f64<1>(t), qcol_f64<2>(t), qcol_f64<3>(t)};
-    double uc[4][NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      uc[0][c] = qcol_f64<0>(u[c]);
-      uc[1][c] = qcol_f64<1>(u[c]);
-      uc[2][c] = qcol_f64<2>(u[c]);
-      uc[3][c] = qcol_f64<3>(u[c]);
-    }
-    // Re = Rb + B'U (upper triangle, mirrored: exactly symmetric) and its inverse
-    double Re[NU][NU], Ri[NU][NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c)
-#pragma unroll
-      for (int d = c; d < NU; ++d) {
-        const double bu = (Bm[0][c] * uc[0][d] + Bm[1][c] * uc[1][d]) + (Bm[2][c] * uc[2][d] + Bm[3][c] * uc[3][d]);
-        Re[c][d] = (R2[c][d] + (c == d ? du[c] : 0.0)) + bu;
-        Re[d][c] = Re[c][d];
-      }
-    ok = spd_inverse<NU>(Re, Ri);
-#pragma unroll
-    for (int c = 0; c < NU; ++c)
-#pragma unroll
-      for (int d = c + 1; d < NU; ++d) Ri[d][c] = Ri[c][d];
-    // L[:, i] and L[:, j] by one formula, L[c][x] = sum_n U[n][c] A[n][x]
-    double Li[NU], Lj[NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      Li[c] = (uc[0][c] * Ai[0] + uc[1][c] * Ai[1]) + (uc[2][c] * Ai[2] + uc[3][c] * Ai[3]);
-      Lj[c] = (uc[0][c] * Aj[0] + uc[1][c] * Aj[1]) + (uc[2][c] * Aj[2] + uc[3][c] * Aj[3]);
-    }
-    // L[:, i]' Re^-1 L[:, j] with (i, j)-symmetric rounding: diagonal terms Ri_cc (Li_c Lj_c),
-    // pairs Ri_cd (Li_c Lj_d + Li_d Lj_c)
-    double corr = 0.0;
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      corr = corr + Ri[c][c] * (Li[c] * Lj[c]);
-#pragma unroll
-      for (int d = c + 1; d < NU; ++d) corr = corr + Ri[c][d] * (Li[c] * Lj[d] + Li[d] * Lj[c]);
-    }
-    const double apa = (Ai[0] * tc[0] + Ai[1] * tc[1]) + (Ai[2] * tc[2] + Ai[3] * tc[3]);
-    const double pn = (qnext + apa) - corr;
-    // mirror the lower triangle
-    const int plo = __builtin_amdgcn_ds_bpermute(tr_addr, __double2loint(pn));
-    const int phi = __builtin_amdgcn_ds_bpermute(tr_addr, __double2hiint(pn));
-    p = i >= j ? pn : __hiloint2double(phi, plo);
-    // gains Kg[:, j] = Re^-1 L[:, j] (row 0 of the wave stores column j), Re^-1 (lane 0)
-    if (lane < 4) {
-#pragma unroll
-      for (int c = 0; c < NU; ++c) {
-        double acc = 0.0;
-#pragma unroll
-        for (int d = 0; d < NU; ++d) acc = acc + Ri[c][d] * Lj[d];
-        s.Kg[(k * NU + c) * 4 + j] = acc;
-      }
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int c = 0; c < NU; ++c)
-#pragma unroll
-        for (int d = 0; d < NU; ++d) s.Ri[(k * NU + c) * NU + d] = Ri[c][d];
-    }
-  }
-  return ok;
-}
+// (Round 4 measured a matrix-core form of the NX = 4, NU <= 2 step — P kept in the result layout of
+// v_mfma_f64_16x16x4_f64, X = P [A | B], [A'; B'] X + [Qb; Rb], P_k = D2 - L'Kg and (P_k + P_k')/2
+// as four dependent matrix instructions plus the 2 x 2 inverse — and did not keep it: correct,
+// but C5 QP 0.740 -> 0.760 ms; a dependent f64 matrix instruction costs ~100 cycles)
 
-// Factorisation: Kg_k and Re_k^-1 for every step into LDS (s.Kg, s.Ri).  Uses s.S (per-step 2x2
-// position weights) and s.DU (input weights).  NX = the state dimension padded to 4 or 8: the
-// model matrices are zero-padded in LDS (setup), so every padded entry of P, T, U, Kg is exactly
-// zero and the loops carry no runtime bounds — every LDS operand of a stage is loaded in one batch.
-// Two wave-local LDS hand-offs per step.  Returns false (uniformly) on a non-positive pivot.
+// Wave 0's part: the recursion (Kg, Ri into LDS; s.sc[62] = 0 on success, 1 on a failed pivot).
+// No barrier: the interior-point loop runs it beside the other waves' work (riccati_factor below
+// is the plain form: this, a barrier, riccati_factor_finish).
 template <int NU, int NX, bool kStationary = false>
-__device__ inline bool riccati_factor(const Lds& s, int H) {
+__device__ inline void riccati_factor_wave0(const Lds& s, int H) {
   const int tid = threadIdx.x, lane = tid & 63;
   double* flag = s.sc + 62;
-#ifdef DRCVAR_MPC_RICCATI_REGS  // measured slower, kept for the record
-  if constexpr (NX == 4 && !kStationary) {  // the register form (above)
-    if (tid < 64) {
-      const bool ok = riccati_factor_regs4<NU>(s, H);
-      if (lane == 0) *flag = ok ? 0.0 : 1.0;
-    }
-  } else
-#endif
   if (tid < 64) {
     constexpr int NX2 = NX * NX;
     const int e = lane < NX2 ? lane : 0;
@@ -939,8 +822,14 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
     }
     if (lane == 0) *flag = ok ? 0.0 : 1.0;
   }
-  __syncthreads();
-  const bool ok = *flag == 0.0;  // uniform
+}
+
+// After a barrier behind riccati_factor_wave0: its outcome (uniform) and, for NX <= 4, the solve
+// maps.  Every thread calls it.
+template <int NU, int NX>
+__device__ inline bool riccati_factor_finish(const Lds& s, int H) {
+  const int tid = threadIdx.x;
+  const bool ok = s.sc[62] == 0.0;  // uniform
   if constexpr (NX <= 4) {
     if (ok) {  // the solves' maps F_k = A' - Kg_k' B' (row-major [k][r][c] in s.SM), once per factor
       for (int e = tid; e < H * 16; e += static_cast<int>(blockDim.x)) {
@@ -954,6 +843,13 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
     }
   }
   return ok;
+}
+
+template <int NU, int NX, bool kStationary = false>
+__device__ inline bool riccati_factor(const Lds& s, int H) {
+  riccati_factor_wave0<NU, NX, kStationary>(s, H);
+  __syncthreads();
+  return riccati_factor_finish<NU, NX>(s, H);
 }
 
 // Solve K x = b with the factorisation above; b in x[0..n) (LDS), overwritten by the solution.
@@ -1669,13 +1565,22 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // f = F1 x0 - F2 xr, summed in this order on purpose: splitting the sum (as the Gp'z sums are)
   // moved the rounding of f enough to stall one degenerate test problem (generic1, H = 64) at
   // merit 1e-8 with a failing polish (degenerate active sets defeat the polish)
+  // (the row of F2 is loaded 16 doubles at a time, all in flight, ahead of the chain: one thread
+  // per row, so the row's ~H nx loads used to sit on the dependent chain one round trip at a time)
   for (int j = tid; j < n; j += kBlock) {
     const double* f1 = a.blob + a.off.F1 + static_cast<int64_t>(j) * nx;
     const double* f2 = a.blob + a.off.F2 + static_cast<int64_t>(j) * H * nx;
     double acc = 0.0;
     for (int q = 0; q < nx; ++q) acc += f1[q] * x0[q];
-    for (int t = 0; t < H; ++t)
-      for (int q = 0; q < nx; ++q) acc -= f2[t * nx + q] * s.xs[t * nx + q];
+    const int len = H * nx;  // f2[t nx + q] in (t, q) order, as the nested loop summed it
+    for (int e0 = 0; e0 < len; e0 += 16) {
+      double fv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) fv[e] = e0 + e < len ? f2[e0 + e] : 0.0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (e0 + e < len) acc -= fv[e] * s.xs[e0 + e];
+    }
     s.f[j] = acc;
   }
   // starting inputs: the tracking optimum without rows, u = -H0^-1 f = UF1 x0 + UF2 xr (condensed
@@ -1773,11 +1678,12 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   }
   double fmaxv = 0.0;
   for (int j = tid; j < n; j += kBlock) fmaxv = fmax(fmaxv, fabs(s.f[j]));
-  if constexpr (CL) {  // |g| over every workgroup's rows (the bound terms are replicated: max)
-    const int ops[1] = {kOpMax};
-    MPC_PHASE(0);
-    cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &gmax, ops, kSiteStart);
-    MPC_PHASE(16);  // cluster exchange
+  if constexpr (CL) {  // |g| over every row of the problem: each workgroup reads all of hs_g (a
+    // cluster exchange before round 4; a maximum is exact in any order, so every workgroup agrees)
+    if (lane < K) {
+      for (int o = wave; o < O; o += kWaves)
+        gmax = fmax(gmax, fabs(a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk]));
+    }
   }
   {
     double unused = 0.0;
@@ -1909,16 +1815,23 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
       }
       __syncthreads();
-      // dual residual of the inputs: r_du = H0 u + f + Gp' v + (lUu - lUl)
-      gpt_parts<NU, kBlock>(s, s.v, H0, s.u, s.red, n, H);
-      __syncthreads();
-      for (int j = tid; j < n; j += kBlock) {
-        double r = s.f[j] + parts_total<kBlock>(s.red, j);
-        if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
-        s.rdu[j] = r;
-        rdm = fmax(rdm, fabs(r));
+      // Wave 0 factorises K (it needs S and DU only) while the other waves form the dual residual
+      // of the inputs r_du = H0 u + f + Gp' v + (lUu - lUl) and the affine rhs dua, one thread per
+      // input (gpt_row: the partial-sum order of gpt_parts).  The factorisation is speculative:
+      // on the iteration whose merit meets the tolerance it is not used (round 4: it used to wait
+      // for those two Gp' products and their three barriers).
+      if (wave == 0) {
+        riccati_factor_wave0<NU, NX>(s, H);
+      } else {
+        for (int j = tid - 64; j < n; j += kBlock - 64) {
+          double r = s.f[j] + gpt_row<NU, kBlock>(s, s.v, H0, s.u, j, n, H);
+          if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
+          s.rdu[j] = r;
+          rdm = fmax(rdm, fabs(r));
+          s.dua[j] = -r - s.rU[j] - gpt_row<NU, kBlock>(s, s.za, nullptr, nullptr, j, n, H);
+        }
       }
-      block_sum_max_max<kWaves>(gap, rpm, rdm, s.sc);
+      block_sum_max_max<kWaves>(gap, rpm, rdm, s.sc);  // its barriers also end the factorisation
       mu = m_ineq > 0.0 ? gap / m_ineq : 0.0;
       rp = rpm;
       rd = rdm;
@@ -1943,15 +1856,12 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     const double gap = mu * m_ineq;
     MPC_PHASE(1);
 
-    // ---- factor K = H0 + diag(DU) + sum_k Mp' S_k Mp (Riccati), affine rhs ----
-    gpt_parts<NU, kBlock>(s, s.za, nullptr, nullptr, s.red, n, H);
-    __syncthreads();
-    for (int j = tid; j < n; j += kBlock) s.dua[j] = -s.rdu[j] - s.rU[j] - parts_total<kBlock>(s.red, j);
-    __syncthreads();
+    // ---- factor K = H0 + diag(DU) + sum_k Mp' S_k Mp (Riccati; wave 0 ran the recursion above,
+    // beside the affine rhs) ----
     MPC_PHASE(2);
     // A failed pivot close to the optimum hands over to the polish (the usual end of a solve
     // whose barrier weights have outgrown fp64); further out the stationary form takes over.
-    if (!riccati_factor<NU, NX>(s, H) &&
+    if (!riccati_factor_finish<NU, NX>(s, H) &&
         (best_merit <= kPolishMerit || !riccati_factor<NU, NX, true>(s, H))) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
@@ -2300,10 +2210,15 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       if (!riccati_factor<NU, NX>(s, H) && !riccati_factor<NU, NX, true>(s, H)) break;
       CL_NOTE(s.Ri[0]);
       MPC_PHASE(11);
+      // The rhs of a pass depends on the multipliers only (the bb terms are at the free response
+      // c), so the multiplier update of pass t also sums pass t + 1's rhs rows, and one exchange
+      // carries both its residual maximum and those sums (`carried`): one cluster exchange per
+      // pass instead of two, the same sums in the same order.
+      bool carried = false;
       for (int pass = 0; pass < kPolishIters; ++pass) {
         // rhs = -f - sum_pen (50 + 100 b) a - E'(nu - rho e), per step through Gp'
         double acc[2] = {0, 0};
-        if (lane < K) {
+        if (!carried && lane < K) {
           const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
           for (int o = o_lo + wave; o < o_hi; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
@@ -2316,15 +2231,17 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
             acc[1] += coef * h1;
           }
         }
-        if constexpr (CL) {
-          MPC_PHASE(12);
-          cluster_combine<kWaves, 2, 0>(cl, s, acc, kOpSum, nullptr, nullptr, kSitePolishRhs);
-          MPC_PHASE(16);  // cluster exchange
-          if (cl.aborted) break;
-        } else {
-          s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];
-          s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
-          __syncthreads();
+        if (!carried) {
+          if constexpr (CL) {
+            MPC_PHASE(12);
+            cluster_combine<kWaves, 2, 0>(cl, s, acc, kOpSum, nullptr, nullptr, kSitePolishRhs);
+            MPC_PHASE(16);  // cluster exchange
+            if (cl.aborted) break;
+          } else {
+            s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];
+            s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
+            __syncthreads();
+          }
         }
         if (wave == 0 && lane < H) {
 #pragma unroll
@@ -2356,17 +2273,29 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
         MPC_PHASE(13);
-        // multiplier updates nu += rho * (E u - e); eres = |E u - e|_inf
+        // multiplier updates nu += rho * (E u - e); eres = |E u - e|_inf; and the next pass's rhs
+        // rows (acc, with the updated multipliers)
         double eres = 0.0;
+        acc[0] = acc[1] = 0.0;
         if (lane < K) {
           const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+          const double c0 = s.c[2 * lane], c1 = s.c[2 * lane + 1];
           for (int o = o_lo + wave; o < o_hi; o += kWaves) {
             const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
-            if (rows.wA[r] == 2.0) {
-              const double e = rows.h0[r] * p0 + rows.h1[r] * p1 + rows.g[r];
-              rows.s[r] += kPolishRho * e;
+            const double flag = rows.wA[r];
+            const double h0 = rows.h0[r], h1 = rows.h1[r], g = rows.g[r];
+            double nu = rows.s[r];
+            if (flag == 2.0) {
+              const double e = h0 * p0 + h1 * p1 + g;
+              nu += kPolishRho * e;
+              rows.s[r] = nu;
               eres = fmax(eres, fabs(e));
             }
+            const double bb = h0 * c0 + h1 * c1 + g;
+            const double coef = flag == 1.0 ? kSlackLin + kSlackHess * bb
+                                            : (flag == 2.0 ? nu + kPolishRho * bb : 0.0);
+            acc[0] += coef * h0;
+            acc[1] += coef * h1;
           }
         }
         if (a.has_u) {
@@ -2400,13 +2329,18 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         if constexpr (CL) {  // every workgroup's equality rows (the bound terms: replicated)
           const int ops[1] = {kOpMax};
           MPC_PHASE(12);
-          cluster_combine<kWaves, 0, 1>(cl, s, nullptr, kOpSum, &eres, ops, kSitePolishEq);
+          cluster_combine<kWaves, 2, 1>(cl, s, acc, kOpSum, &eres, ops, kSitePolishEq);
           MPC_PHASE(16);  // cluster exchange
+          if (cl.aborted) break;
+        } else {
+          s.red[(wave * kPerStepQ) * 64 + lane] = acc[0];  // published by the barriers below
+          s.red[(wave * kPerStepQ + 1) * 64 + lane] = acc[1];
         }
         double unused_a = 0.0, unused_b = 0.0;
         block_sum_max_max<kWaves>(unused_a, eres, unused_b, s.sc);  // uniform; also the barrier
         CL_NOTE(eres);
         if (eres <= kPolishEqTol * scale_d) break;
+        carried = true;
       }
       // sign conditions; violators move (primal-dual active-set step).  Rows that must become
       // equalities (a dropped row violated, a penalised row with s < 0) and equalities with a

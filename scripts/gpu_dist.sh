@@ -14,7 +14,9 @@ d = json.loads(sys.stdin.read())
 print($1, 'metric', round(d['value']), d['ms_per_step'], d['config']['parallelism'], d['scaling'])
 for w, s in (d.get('strong_scaling') or {}).items():
     print($1, 'strong', w, round(s['value']), round(s['ms_per_step'], 4), s['parallelism'], s['units_per_rank'],
-          s['phases_rank_max'], s['launch'], s.get('full_loop', {}).get('ms_per_step'))"
+          s['phases_rank_max'], s['launch'], s.get('full_loop', {}).get('ms_per_step'))
+    if s.get('pipelined'):
+        print($1, 'strong', w, 'pipelined', s['pipelined'])"
 }
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29502 bench.py --gpus 2 --steps 400 --warmup 50 --dist-backend gloo --no-cpu-baseline \

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=["30,3,1", "30,3,3", "30,3,1024", "20,10,3",
                                                     "50,256,1", "50,256,3"])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tol", type=float, default=mf.DEFAULT_TOL, help="interior-point tolerance")
     ap.add_argument("--cluster", type=int, default=0,
                     help="workgroups per problem (drcvar_mpc_options.cluster_size; 0 = automatic, 1 = one)")
     args = ap.parse_args()
@@ -61,16 +62,20 @@ def main():
         model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
         h, g = rec[..., 3:5], rec[..., 7]
         ws = torch.empty(model.workspace_doubles(B, O), dtype=torch.float64, device=dev)
-        x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt)
+        x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt, tol=args.tol)
         torch.cuda.synchronize()
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record()
         for _ in range(args.reps):
-            x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt)
+            x, u, info = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt, tol=args.tol)
         t1.record()
         torch.cuda.synchronize()
         ms = t0.elapsed_time(t1) / args.reps
         inf = info.cpu().numpy()
+        du_ref = float("nan")
+        if args.tol != mf.DEFAULT_TOL:  # the answer against the default tolerance's
+            u_ref = mf.filter_batch(model, h, g, x0, xr, uf, workspace=ws, options=opt)[1]
+            du_ref = float((u - u_ref).abs().max())
         st = inf[:, _native.MPC_INFO_STATUS]
         print(f"H={H} O={O} B={B} groups={model.launch_groups(B, O, opt)}: {ms:.3f} ms/launch, "
               f"{B / ms * 1e3:.0f} QPs/s, "
@@ -79,7 +84,8 @@ def main():
               f"max polish attempts {inf[:, _native.MPC_INFO_POLISH_ATTEMPTS].max():.0f}, "
               f"polished {inf[:, _native.MPC_INFO_POLISHED].mean():.2f}, "
               f"polish attempts {inf[:, _native.MPC_INFO_POLISH_ATTEMPTS].mean():.2f}, "
-              f"optimal {(st == 0).mean():.2f}, fallback {inf[:, _native.MPC_INFO_USED_FALLBACK].mean():.2f}",
+              f"optimal {(st == 0).mean():.2f}, fallback {inf[:, _native.MPC_INFO_USED_FALLBACK].mean():.2f}, "
+              f"tol {args.tol:.0e} max|u - u(default tol)| {du_ref:.1e}",
               flush=True)
 
 
