@@ -47,106 +47,7 @@ constexpr int kBlock = 256;
 // kernel (rocprofv3 counters, profiles/r03/sampler_pmc_pairs2.json); 8 per thread keep the SIMDs fed.
 constexpr int kPairs = 8;
 
-#include "drcvar_sampling_tables.inc"
-
-struct Philox {
-  uint32_t x[4];
-};
-
-__device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                                uint32_t k0, uint32_t k1) {
-  constexpr uint64_t kM0 = 0xD2511F53u, kM1 = 0xCD9E8D57u;
-  constexpr uint32_t kW0 = 0x9E3779B9u, kW1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = kM0 * c0, p1 = kM1 * c2;  // one v_mad_u64_u32 each
-    uint32_t n0, n2;  // hi(p1) ^ c1 ^ k0, hi(p0) ^ c3 ^ k1 (the key words are uniform: SGPRs)
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(static_cast<uint32_t>(p1 >> 32)), "v"(c1), "s"(k0));
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(static_cast<uint32_t>(p0 >> 32)), "v"(c3), "s"(k1));
-    c0 = n0;
-    c1 = static_cast<uint32_t>(p1);
-    c2 = n2;
-    c3 = static_cast<uint32_t>(p0);
-    // The key schedule is bumped in SALU each round (volatile: otherwise all twenty round keys are
-    // hoisted out of the sample loop, spilled to VGPR lanes and read back with one v_readlane per
-    // use — VALU work in a VALU-bound kernel).
-    asm volatile("s_add_u32 %0, %0, %1" : "+s"(k0) : "s"(kW0) : "scc");
-    asm volatile("s_add_u32 %0, %0, %1" : "+s"(k1) : "s"(kW1) : "scc");
-  }
-  return Philox{{c0, c1, c2, c3}};
-}
-
-// fma with a uniform third operand held in SGPRs (the polynomial coefficients): as v_fma_f64 with
-// an SGPR source instead of the compiler's v_mov_b64 of a VGPR-held coefficient + v_fmac_f64 —
-// one VALU instruction per Horner step instead of two.  Same IEEE fma, same bits.
-__device__ __forceinline__ double fma_sc(double a, double b, double c) {
-  double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
-  return r;
-}
-
-// -2 log u for the uniform u = (x + 1/2) 2^-32 in the open interval (0, 1) of a 32-bit word (at
-// most 33 significant bits: exact, in [2^-33, 1 - 2^-33], never 0 or 1).  It is formed as
-// w = 2x + 1 (one fma with inline constants, exact) and u = w 2^-33, folded into the exponent.
-// u = m 2^e, m in [1/2, 1); the top 9 mantissa bits, rounded, pick the nearest centre
-// c_k = 1/2 + k/512 (k = 0..256; c_256 = 1 exactly, so log u keeps its relative accuracy as u -> 1);
-// r = m (1/c_k) - 1 (|r| <= 1/512 + 2^-52); log m = log1p(r) - log(1/c_k),
-// log1p(r) = r + r^2 P(r), P to r^4 (the next term, r^7 / 7, is below 2^-56 of r).
-// The factor -2 of Box-Muller is folded in exactly: the LDS table holds -2/c_k and 2 log(1/c_k)
-// (indexed by the 9 bits themselves, each centre stored for both of its indices), the fma gives
-// r2 = -2r, the Horner coefficients are those of P scaled by powers of two so that the sum is
-// -P/2 in r2, and -2 log1p(r) = r2 + r2^2 (-P/2).  Every step is the unscaled step times a power
-// of two, so the result is bitwise -2 times the unscaled evaluation (what the host mirror,
-// oracle/philox_sampler.py, computes) — one multiply less.
-__device__ __forceinline__ double neg2_log_u32(uint32_t x, const double* log_t) {
-  const double w = fma(static_cast<double>(x), 2.0, 1.0);
-  const double m = __builtin_amdgcn_frexp_mant(w);
-  const int e = __builtin_amdgcn_frexp_exp(w) - 33;
-  const uint32_t idx = __builtin_amdgcn_ubfe(static_cast<uint32_t>(__double2hiint(m)), 11, 9);
-  const double ninv2 = log_t[2 * idx], log_inv2 = log_t[2 * idx + 1];  // -2/c_k, 2 log(1/c_k)
-  const double r2 = fma(m, ninv2, 2.0);                                 // -2 r
-  double q = (-1.0 / 6.0) * (-1.0 / 32.0);
-  q = fma_sc(q, r2, (1.0 / 5.0) * (1.0 / 16.0));
-  q = fma_sc(q, r2, (-1.0 / 4.0) * (-1.0 / 8.0));
-  q = fma_sc(q, r2, (1.0 / 3.0) * (1.0 / 4.0));
-  q = fma_sc(q, r2, (-1.0 / 2.0) * (-1.0 / 2.0));                     // -P(r) / 2
-  const double m2log1p = fma(r2 * r2, q, r2);                           // -2 log1p(r)
-  constexpr double kLn2Hi = 0x1.62e42fefa3800p-1, kLn2Lo = 0x1.ef35793c76730p-45;
-  const double de = static_cast<double>(e);
-  return fma(de, -2.0 * kLn2Hi, fma(de, -2.0 * kLn2Lo, log_inv2 + m2log1p));
-}
-
-// sqrt(-2 log u).  The argument is >= 2^-33 ln 4 > 0, never denormal, so rsq + two Newton-Raphson
-// steps (Goldschmidt form) replace the library sqrt and its rescaling.
-__device__ __forceinline__ double box_muller_radius(uint32_t x, const double* log_t) {
-  const double y = neg2_log_u32(x, log_t);
-  const double rs = __builtin_amdgcn_rsq(y);
-  double h = 0.5 * rs, r = y * rs;
-  const double e = fma(-r, h, 0.5);
-  r = fma(r, e, r);
-  h = fma(h, e, h);
-  return fma(fma(-r, r, y), h, r);
-}
-
-// (cos, sin)(2 pi w / 2^32): table point k = round(w / 2^23) mod 512 (32-bit wrap-around), signed
-// remainder rem = w - k 2^23 in [-2^22, 2^22), b = 2 pi rem / 2^32 in [-pi/512, pi/512);
-// sin b = b + b^3 (-1/6 + b^2/120) (next term b^7/5040: 1e-17 of b), cos b - 1 = b^2 (-1/2 + b^2/24)
-// (next term b^6/720 < 8e-17), and (cos, sin)(a + b) = (C (1 + cm1) - S sb, S (1 + cm1) + C sb)
-// with (C, S) = kTurn[k].
-__device__ __forceinline__ void cos_sin_u32(uint32_t w, const double* turn, double* cs, double* sn) {
-  const uint32_t k = (w + (1u << 22)) >> 23;
-  const int32_t rem = __builtin_amdgcn_sbfe(static_cast<int32_t>(w), 0, 23);  // = w - k 2^23
-  constexpr double kTurn32 = 6.28318530717958647692 * 0x1.0p-32;
-  const double b = static_cast<double>(rem) * kTurn32;
-  const double z = b * b;
-  const double ps = fma_sc(z, 1.0 / 120.0, -1.0 / 6.0);
-  const double sb = fma(b * z, ps, b);
-  const double pc = fma_sc(z, 1.0 / 24.0, -0.5);
-  const double cm1 = z * pc;
-  const double C = turn[2 * k], S = turn[2 * k + 1];
-  *cs = fma(C, cm1, fma(-S, sb, C));
-  *sn = fma(S, cm1, fma(C, sb, S));
-}
+#include "drcvar_generator.inc"
 
 // Units [u0, u0 + count) of the global [O, T] grid (u = o T + t); unit u is written at
 // out + (o - o0) so + (t - t0) st with (o0, t0) = divmod(u0, T), so a whole [O, T, N, 2] batch
@@ -189,18 +90,8 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
   // The tables are read from LDS, not from global memory: a global table load is counted by
   // vmcnt together with the wave's earlier sample stores, and waiting for the load (in order)
   // would wait for those stores' write acknowledgements too, serialising arithmetic and stores.
-  constexpr int kTurnLen = sizeof(kTurn) / sizeof(double);
-  constexpr int kLogIdx = 2 * (sizeof(kLogT) / sizeof(double) / 2 - 1);  // 512 nine-bit indices
   __shared__ double s_turn[kTurnLen], s_log[2 * kLogIdx];
-  for (int i = threadIdx.x; i < kTurnLen + kLogIdx; i += kBlock) {
-    if (i < kTurnLen) {
-      s_turn[i] = kTurn[i];
-    } else {  // index j -> centre (j + 1) / 2, scaled by -2 (exact)
-      const int j = i - kTurnLen, c = (j + 1) >> 1;
-      s_log[2 * j] = -2.0 * kLogT[2 * c];
-      s_log[2 * j + 1] = -2.0 * kLogT[2 * c + 1];
-    }
-  }
+  load_generator_tables(s_turn, s_log, kBlock);
   __syncthreads();
   const int64_t pairs = (a.N + 1) >> 1;  // Philox calls per unit
   for (int64_t k = blockIdx.y; k < a.count; k += gridDim.y) {

@@ -24,4 +24,7 @@ print("value", round(d["value"] / 1e6, 2), "M/s  ms_per_step", round(d["ms_per_s
       "| C5 full", round(m["full_loop_c5"]["full_step_ms"], 4), "qp", round(m["full_loop_c5"]["qp_ms"], 4), m["full_loop_c5"]["qp_iterations"],
       "err_u", m["full_loop_c5"].get("max_abs_err_u_vs_oracle"), "| main_flow", round(m["main_flow_c5"]["step_ms"], 4), m["main_flow_c5"]["qp_iterations"],
       "| batched", round(m["batched_reference"]["launch_ms"], 4), "| max_abs_err", d.get("max_abs_err"))
+sm = d["sampling"]
+print("sampler", round(sm["kernel_ms"], 4), "ms; C5 evaluate", round(d["roofline_large"]["kernel_ms"], 4),
+      "ms; fused draw+evaluate", sm["fused_draw_evaluate"])
 PY
