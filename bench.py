@@ -462,6 +462,51 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload)
                             "qp": f"dr_cvar safety filter, H={T}, {sb.U} halfspace rows, one problem, "
                                   f"replicated on every rank",
                             "qp_status": mf.STATUS_NAMES.get(int(info[0])), "qp_iterations": int(info[1])}
+        # main.py's whole flow per step (main.py:95-112): the halfspaces, then its THREE safety
+        # filters (mean, CVaR, DR-CVaR) — independent QPs over the same records, distributed over
+        # the ranks (rank r solves metrics[r::world]; one rank: all three in one launch), then one
+        # all-gather of the filtered inputs so every rank holds every filter's answer
+        metrics = ("mean", "cvar", "dr_cvar")
+        mine = metrics[rank::world]
+        nb = len(mine)
+        slots = -(-len(metrics) // world)
+        ws3 = h3 = g3 = None
+        if nb:
+            cols_h = torch.tensor([c for m in mine for c in (mf.METRIC_COLUMNS[m][0], mf.METRIC_COLUMNS[m][0] + 1)],
+                                  device=dev)
+            cols_g = torch.tensor([mf.METRIC_COLUMNS[m][1] for m in mine], device=dev)
+            x0m, xrm, ufm = (x0.expand(nb, -1).contiguous(), xr.expand(nb, -1, -1).contiguous(),
+                             uf.expand(nb, -1, -1).contiguous())
+            ws3 = torch.empty(model.workspace_doubles(nb, O), dtype=torch.float64, device=dev)
+        usend = torch.zeros((slots, T, 2), dtype=torch.float64, device=dev)
+        ufull = (torch.empty((slots * world, T, 2), dtype=torch.float64, device=gdev or dev)
+                 if world > 1 else None)
+
+        def flow(k):
+            for _ in range(k):
+                sb.step()
+                if sb.full is not None and sb.full.device != dev:
+                    rec.copy_(sb.records())
+                if nb:
+                    hm = rec.index_select(2, cols_h).view(O, T, nb, 2).permute(2, 0, 1, 3)
+                    gm = rec.index_select(2, cols_g).permute(2, 0, 1)
+                    u, info3 = mf.filter_batch(model, hm, gm, x0m, xrm, ufm, workspace=ws3)[1:]
+                    usend[:nb].copy_(u)
+                    res["info3"] = info3
+                if ufull is not None:
+                    sharding._all_gather(ufull, usend)
+            return k
+
+        flow(2)
+        el3, _, _ = timed(world, lambda: flow(Kf), dev, stream)
+        inf3 = res["info3"].cpu().numpy() if nb else np.zeros((0, 10))
+        out["main_flow"] = {"steps": Kf, "ms_per_step": el3 / Kf * 1e3,
+                            "what": "main.py's three safety filters (mean, CVaR, DR-CVaR) per step over "
+                                    f"the sharded halfspaces; rank r solves {list(metrics)}[r::{world}], then "
+                                    "an all-gather of the filtered inputs",
+                            "rank0_filters": list(mine),
+                            "rank0_qp_iterations": [int(v) for v in inf3[:, 1]],
+                            "rank0_qp_status": [mf.STATUS_NAMES.get(int(v)) for v in inf3[:, 0]]}
     if rank == 0 and world == 1 and workload == "c5":
         out["_batch"] = sb
         large = roofline(sb.algorithmic_bytes, kernel_s, load_traffic("c5"))

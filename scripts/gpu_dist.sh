@@ -16,7 +16,9 @@ for w, s in (d.get('strong_scaling') or {}).items():
     print($1, 'strong', w, round(s['value']), round(s['ms_per_step'], 4), s['parallelism'], s['units_per_rank'],
           s['phases_rank_max'], s['launch'], s.get('full_loop', {}).get('ms_per_step'))
     if s.get('pipelined'):
-        print($1, 'strong', w, 'pipelined', s['pipelined'])"
+        print($1, 'strong', w, 'pipelined', s['pipelined'])
+    if s.get('main_flow'):
+        print($1, 'strong', w, 'main_flow', s['main_flow']['ms_per_step'], s['main_flow']['rank0_filters'], s['main_flow']['rank0_qp_iterations'])"
 }
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29502 bench.py --gpus 2 --steps 400 --warmup 50 --dist-backend gloo --no-cpu-baseline \
