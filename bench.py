@@ -75,6 +75,25 @@ def load_traffic(workload):
         return None
 
 
+def load_rocprof(workload, abytes):
+    """The same kernel's average dispatch time in the committed rocprofv3 kernel trace of this
+    command (profiles/rocprof_kernel_time.json, scripts/rocprof_kernel_time.py), with the frac it
+    gives: the profile-consistent companion of the event-timed `frac` (the profiler's per-dispatch
+    completion signals stretch back-to-back graph dispatches, so it reads lower)."""
+    path = os.path.join(REPO, "profiles", "rocprof_kernel_time.json")
+    try:
+        with open(path) as f:
+            e = json.load(f).get(workload)
+    except (OSError, ValueError):
+        return None
+    if not e:
+        return None
+    return {"file": e["file"], "kernel": e["kernel"], "command": e["command"],
+            "dispatches": e["dispatches"], "kernel_ms": e["mean_ns"] * 1e-6,
+            "achieved": abytes / (e["mean_ns"] * 1e-9) / 1e9,
+            "frac": abytes / (e["mean_ns"] * 1e-9) / HBM_PEAK}
+
+
 def roofline(abytes, kernel_s, traffic):
     achieved = abytes / kernel_s
     return {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
@@ -328,7 +347,8 @@ def main():
                        "launch": stepper.describe(),
                        "alpha": params.alpha, "delta": params.delta, "epsilon": params.epsilon},
             "roofline": dict(roofline(sb.algorithmic_bytes, kernel_s, load_traffic(args.workload)),
-                             timing=ktiming),
+                             timing=ktiming,
+                             rocprof=load_rocprof(args.workload, sb.algorithmic_bytes)),
             "strong_scaling": strong,
         }
     large = mpc = sampling = None

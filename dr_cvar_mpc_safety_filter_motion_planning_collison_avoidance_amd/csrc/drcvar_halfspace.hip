@@ -41,6 +41,7 @@ constexpr int kWave = 64;
 constexpr int kCap = 128;          // candidates ranked directly (per-wave region size in LDS)
 constexpr int kMaxValueIters = 3;  // value-linear refinements before switching to integer keys
 constexpr double kSentinel = 100.0;
+constexpr int kPairMax = 12288;  // generating plans up to this many slots draw in pairs (LDS staging)
 // sample load forms (kernel template); kLoadGen: no loads, the samples are drawn in registers
 constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2, kLoadGen = 3;
 #ifndef DRCVAR_NT_BYTES  // diagnostic builds may move the threshold (scripts/micro A/B runs)
@@ -788,6 +789,79 @@ __device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, d
   }
 }
 
+#ifdef DRCVAR_DIAG_BITONIC
+// Diagnostic build (round 4): the price of the first half of a single-barrier
+// selection — each wave sorting its own 64 P projections in registers (bitonic network over the
+// element index e = 64 r + lane: partners in other registers for strides >= 64, otherwise lane
+// xor j through quad DPP (1, 2), ds_swizzle (4), row_ror:8 (8), permlane16/32_swap (16, 32); the
+// P registers of a stage are interleaved so their chains fill each other's hazard slots).  The
+// rest of the kernel is unchanged (it reads d[] as a multiset), so the stamps' phase 2 grows by
+// exactly the sort.
+template <int J>
+__device__ __forceinline__ double lane_xor_f64(double v) {
+  if constexpr (J == 1) {
+    return dpp_f64<kDppQuadXor1>(v);
+  } else if constexpr (J == 2) {
+    return dpp_f64<kDppQuadXor2>(v);
+  } else if constexpr (J == 4) {
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x1F | (4 << 10));
+    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x1F | (4 << 10));
+    return __hiloint2double(hi, lo);
+  } else {
+    static_assert(J == 8);
+    return dpp_f64<0x128>(v);  // row_ror:8 = lane xor 8 within a row of 16
+  }
+}
+template <int P, int K, int J>
+__device__ __forceinline__ void bitonic_stage(double (&v)[P], int lane) {
+  if constexpr (J >= kWave) {
+    constexpr int JR = J / kWave;
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      if ((r & JR) == 0) {
+        const bool up = ((r * kWave) & K) == 0;  // K >= 2 J >= 128: a bit of r, uniform
+        const double lo = fmin(v[r], v[r | JR]), hi = fmax(v[r], v[r | JR]);
+        v[r] = up ? lo : hi;
+        v[r | JR] = up ? hi : lo;
+      }
+    }
+  } else {
+    double a[P], b[P];
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      if constexpr (J == 16 || J == 32) {  // {v, partner} = the swap's two results
+        const auto lo = J == 16 ? __builtin_amdgcn_permlane16_swap(__double2loint(v[r]), __double2loint(v[r]), false, false)
+                                : __builtin_amdgcn_permlane32_swap(__double2loint(v[r]), __double2loint(v[r]), false, false);
+        const auto hi = J == 16 ? __builtin_amdgcn_permlane16_swap(__double2hiint(v[r]), __double2hiint(v[r]), false, false)
+                                : __builtin_amdgcn_permlane32_swap(__double2hiint(v[r]), __double2hiint(v[r]), false, false);
+        a[r] = __hiloint2double(hi[0], lo[0]);
+        b[r] = __hiloint2double(hi[1], lo[1]);
+      } else {
+        a[r] = v[r];
+        b[r] = lane_xor_f64<J>(v[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const int e = r * kWave + lane;
+      const bool keep_min = (((e & K) == 0) == ((e & J) == 0));
+      v[r] = keep_min ? fmin(a[r], b[r]) : fmax(a[r], b[r]);
+    }
+  }
+}
+template <int P, int K, int J>
+__device__ __forceinline__ void bitonic_merge(double (&v)[P], int lane) {
+  bitonic_stage<P, K, J>(v, lane);
+  if constexpr (J > 1) bitonic_merge<P, K, J / 2>(v, lane);
+}
+template <int P, int K = 2>
+__device__ __forceinline__ void wave_bitonic_sort(double (&v)[P], int lane) {
+  static_assert((P & (P - 1)) == 0, "power-of-two registers");
+  bitonic_merge<P, K, K / 2>(v, lane);
+  if constexpr (K < P * kWave) wave_bitonic_sort<P, 2 * K>(v, lane);
+}
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
 //   BLOCK    threads per unit (one workgroup per unit)
@@ -884,6 +958,37 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     }
   };
   double x[P], y[P];
+  // Paired draws (plans with BLOCK P <= kPairMax): one Philox call gives samples i and i + pairs
+  // (pairs = ceil(N/2)); the thread holding i < pairs draws both, keeps i and hands i + pairs to
+  // its owner through LDS (extern staging [pairs] of 16 B, one barrier) — half the Philox work of
+  // one call per sample, the same values.
+  constexpr bool kPaired = kGen && BLOCK * P <= kPairMax;
+  extern __shared__ dbl2 gen_stage[];
+  if constexpr (kPaired) {
+    if (!gzero) {
+      const int pairs = static_cast<int>(gen.pairs);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < pairs) {
+          double x2, y2;
+          generate_pair(gg0, i, gen.s0, gen.s1, gen.k0, gen.k1, gnx, gny, gen.l00, gen.l10,
+                        gen.l11, s_turn, s_log, &x[j], &y[j], &x2, &y2);
+          if (i + pairs < n) gen_stage[i] = dbl2{x2, y2};
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i >= pairs) {
+          const dbl2 v = gen_stage[(i < n ? i : n - 1) - pairs];
+          x[j] = v.x;
+          y[j] = v.y;
+        }
+      }
+    }
+  }
   const int64_t off0 = static_cast<int64_t>(tid) * s_samp;
   const int64_t row_step = static_cast<int64_t>(BLOCK) * s_samp;
   const int64_t off_last = static_cast<int64_t>(n - 1) * s_samp;
@@ -891,7 +996,12 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   for (int j = 0; j < P; ++j) {
     const int i = tid + j * BLOCK;
     const int64_t off = i < n ? off0 + j * row_step : off_last;
-    if constexpr (kGen) {  // drawn, not loaded (idle slots draw sample n - 1, as they would load it)
+    if constexpr (kPaired) {  // drawn above (gzero: the nominal point)
+      if (gzero) {
+        x[j] = gnx;
+        y[j] = gny;
+      }
+    } else if constexpr (kGen) {  // drawn, not loaded (idle slots draw sample n - 1, as they would load it)
       draw(i < n ? i : n - 1, &x[j], &y[j]);
     } else if constexpr (LOAD == kLoadNt) {  // streamed once: keep it out of L2 / MALL
       const dbl2 v = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(base + off));
@@ -997,6 +1107,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 #pragma unroll
   for (int j = 0; j < P; ++j)  // +inf padding: never below, inside or a candidate
     d[j] = (tid + j * BLOCK < n) ? project(h0, h1, x[j], y[j]) : INFINITY;
+#ifdef DRCVAR_DIAG_BITONIC
+  if constexpr ((P & (P - 1)) == 0) wave_bitonic_sort<P>(d, lane);
+#endif
   const double mu_d = h0 * mux + h1 * muy;
   double var_d;
   if constexpr (kPilot) {  // variance of the pilot's projections about the exact mean, in fp32
@@ -1187,7 +1300,11 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       double lo[1] = {INFINITY}, hi[1] = {-INFINITY};
 #pragma unroll
       for (int j = 0; j < P; ++j) {
+#ifdef DRCVAR_DIAG_BITONIC
+        if (d[j] != INFINITY) {  // sorted: the padding sits at the end of the wave's order
+#else
         if (tid + j * BLOCK < n) {
+#endif
           lo[0] = fmin(lo[0], d[j]);
           hi[0] = fmax(hi[0], d[j]);
         }
@@ -1368,11 +1485,23 @@ constexpr int64_t kMaxGridY = 65535;
 template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
 void launch_form(const Launch& L) {
   const int64_t n_obs = L.units / L.n_steps;
+  size_t dyn = DRCVAR_HS_LDS_PAD;
+  if constexpr (LOAD == kLoadGen && BLOCK * P <= kPairMax) {
+    // the paired draws' staging: [pairs] of 16 B (80 KB at N = 10 000: above the default 64 KB
+    // limit of dynamic LDS, raised once per kernel)
+    dyn = static_cast<size_t>(L.gen.pairs) * 16;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kPairMax / 2 * 16));
+      attr_set = true;
+    }
+  }
   for (int64_t o0 = 0; o0 < n_obs; o0 += kMaxGridY) {
     const int64_t chunk = n_obs - o0 < kMaxGridY ? n_obs - o0 : kMaxGridY;
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
                        dim3(static_cast<unsigned>(L.n_steps), static_cast<unsigned>(chunk)),
-                       dim3(BLOCK), DRCVAR_HS_LDS_PAD, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
+                       dim3(BLOCK), dyn, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
                        static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
                        L.dir + o0 * L.dir_s_obs, L.dir_s_obs, L.dir_s_step, L.prm,
                        L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH,
