@@ -41,7 +41,10 @@ constexpr int kWave = 64;
 constexpr int kCap = 128;          // candidates ranked directly (per-wave region size in LDS)
 constexpr int kMaxValueIters = 3;  // value-linear refinements before switching to integer keys
 constexpr double kSentinel = 100.0;
-constexpr int kPairMax = 12288;  // generating plans up to this many slots draw in pairs (LDS staging)
+#ifndef DRCVAR_PAIR_MAX  // diagnostic builds may move it (0: every slot its own Philox call)
+#define DRCVAR_PAIR_MAX 12288
+#endif
+constexpr int kPairMax = DRCVAR_PAIR_MAX;  // generating plans up to this many slots draw in pairs (LDS staging)
 // sample load forms (kernel template); kLoadGen: no loads, the samples are drawn in registers
 constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2, kLoadGen = 3;
 #ifndef DRCVAR_NT_BYTES  // diagnostic builds may move the threshold (scripts/micro A/B runs)
