@@ -897,9 +897,19 @@ __device__ __forceinline__ int opaque_wave() {
 constexpr int kBlkSlot = 160;
 constexpr int kBlkMinH = 16;
 #ifdef DRCVAR_BLOCKED
-constexpr bool kBlockedCode = true;  // the blocked factorisation and solve chains (A/B builds)
+constexpr bool kBlockedCode = true;  // the blocked factorisation (A/B builds)
 #else
 constexpr bool kBlockedCode = false;
+#endif
+#ifdef DRCVAR_BLOCKED_SOLVE
+constexpr bool kBlockedSolve = kBlockedCode;  // ... and the blocked solve chains (measured slower)
+#else
+constexpr bool kBlockedSolve = false;
+#endif
+#ifdef DRCVAR_BLOCKED_DYN
+constexpr bool kBlockedDyn = kBlockedCode && !kBlockedSolve;  // rows' H0 u through the dynamics
+#else
+constexpr bool kBlockedDyn = false;
 #endif
 #ifndef DRCVAR_BLK_W
 #define DRCVAR_BLK_W 8
@@ -907,7 +917,7 @@ constexpr bool kBlockedCode = false;
 constexpr int kBlkW = DRCVAR_BLK_W;  // blocks (waves 0..kBlkW-1 of an 8-wave workgroup)
 static_assert(kBlkW >= 3 && kBlkW <= 8, "blocked factorisation: 3..8 blocks");
 constexpr int kBlkRowParts = 4 * 128;  // partial sums of the rows (rhs_parts): n * PARTS <= 480
-static_assert(kBlkW * kBlkSlot + 2 * kBlkRowParts <= 8 * kPerStepQ * 64,
+static_assert(kBlkW * kBlkSlot + 2 * kBlkRowParts + 20 * DRCVAR_MPC_MAX_HORIZON <= 8 * kPerStepQ * 64,
               "blocked factorisation scratch exceeds s.red");
 
 __device__ __forceinline__ int blk_begin(int w, int H) { return (w * H) / kBlkW; }
@@ -941,6 +951,28 @@ __device__ inline void rhs_parts(const Lds& s, const double* H0T, int n, int H, 
         if (l0 + q * PARTS < n) acc += hv[q] * s.u[l0 + q * PARTS];
     }
     psA[j_a * PARTS + part] = acc;
+    psB[j_a * PARTS + part] = acc2;
+  }
+}
+
+// rhs_parts with the H0 u term through the dynamics: psA's part holds (Gp' v) + 2 (Gx' Z) over
+// its k (Z = Q Gx u per step, [H][4], AB[i] = A^i B in s.xs), psB (Gp' za) as rhs_parts.
+template <int NU, int kBlock>
+__device__ inline void rhs_parts_dyn(const Lds& s, int n, int H, double* psA, double* psB,
+                                     const double* Zs, int t, int nt) {
+  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
+  for (int e = t; e < n * PARTS; e += nt) {
+    const int part = e / n, j_a = e - part * n;
+    const int j = j_a / NU, a = j_a - j * NU;
+    double acc = 0.0, acc2 = 0.0, accz = 0.0;
+    for (int k = j + part; k < H; k += PARTS) {
+      const double* m = s.Mp + (k - j) * 2 * NU;
+      acc += m[a] * s.v[2 * k] + m[NU + a] * s.v[2 * k + 1];
+      acc2 += m[a] * s.za[2 * k] + m[NU + a] * s.za[2 * k + 1];
+      const double* ab = s.xs + (k - j) * 4 * NU + a;
+      accz += (ab[0] * Zs[4 * k] + ab[NU] * Zs[4 * k + 1]) + (ab[2 * NU] * Zs[4 * k + 2] + ab[3 * NU] * Zs[4 * k + 3]);
+    }
+    psA[j_a * PARTS + part] = acc + 2.0 * accz;
     psB[j_a * PARTS + part] = acc2;
   }
 }
@@ -1620,7 +1652,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
     W[e] = acc;
   }
   __syncthreads();
-  if constexpr (kBlockedCode && kBlock == 512) {
+  if constexpr (kBlockedSolve && kBlock == 512) {
     if (blk) chain_back_blocked(s, H, W);
   }
   if (!blk && t < 64) {  // backward: p_k = F_k p_{k+1} + w_k, row i of F_k
@@ -1675,7 +1707,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
     }
   }
   __syncthreads();
-  if constexpr (kBlockedCode && kBlock == 512) {
+  if constexpr (kBlockedSolve && kBlock == 512) {
     if (blk) chain_fwd_blocked(s, H, W, G);
   }
   if (!blk && t < 64) {  // forward: x_{k+1} = F_k' x_k + B kff_k, column i of F_k
@@ -2200,6 +2232,24 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     s.u[j] = u0;
   }
   __syncthreads();
+  if constexpr (kBlockedDyn && NX == 4 && kWaves == 8) {
+    // the blocked form's rows take H0 u through the dynamics: AB[i] = A^i B ([H][4][NU] in s.xs,
+    // free from here to the output rollout), by the last wave (first read behind later barriers)
+    if (blocked && wave == kWaves - 1) {
+      const int r = lane / NU, c = lane - (lane / NU) * NU;
+      const bool mine = lane < 4 * NU;
+      double v = mine ? s.Bm[r * NU + c] : 0.0;
+      if (mine) s.xs[lane] = v;
+      for (int i = 1; i < H; ++i) {
+        wave_lds_fence();
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc += s.Am[r * kMx + m] * s.xs[(i - 1) * 4 * NU + m * NU + c];
+        wave_lds_fence();
+        if (mine) s.xs[i * 4 * NU + lane] = acc;
+      }
+    }
+  }
   positions<NU, kBlock>(s, s.u, s.p, s.c, H);
   __syncthreads();
 
@@ -2436,19 +2486,58 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
           // its own block; combined after one barrier
           double* psA = s.red + kBlkW * kBlkSlot;
           double* psB = psA + kBlkRowParts;
+          const bool dyn = kBlockedDyn && 4 * NU * H <= (DRCVAR_MPC_MAX_HORIZON + 1) * DRCVAR_MPC_MAX_STATES;
+          if constexpr (kBlockedDyn) {
+            if (dyn) {  // H0 u = 2 (Gx' Q Gx u + R u): the states Gx u, then Z = Q Gx u (all threads)
+              double* Xp = psB + kBlkRowParts;  // [H][4][4 parts]
+              double* Zs = Xp + 16 * DRCVAR_MPC_MAX_HORIZON;  // [H][4]
+              for (int e = tid; e < 16 * H; e += kBlock) {
+                const int part = e & 3, k = e >> 4, i = (e >> 2) & 3;
+                double acc = 0.0;
+                for (int j = part; j <= k; j += 4) {
+#pragma unroll
+                  for (int c = 0; c < NU; ++c) acc += s.xs[(k - j) * 4 * NU + i * NU + c] * s.u[j * NU + c];
+                }
+                Xp[e] = acc;
+              }
+              __syncthreads();
+              for (int e = tid; e < 4 * H; e += kBlock) {
+                const int k = e >> 2, i = e & 3;
+                double z = 0.0;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                  const double* xp = Xp + (k * 4 + m) * 4;
+                  z += s.Qm[i * kMx + m] * (((xp[0] + xp[1]) + xp[2]) + xp[3]);
+                }
+                Zs[e] = z;
+              }
+              __syncthreads();
+            }
+          }
           ric_blocked_phase1<NU>(s, H);
+          if constexpr (kBlockedDyn) {
+            if (dyn && wave == 0)
+              rhs_parts_dyn<NU, kBlock>(s, n, H, psA, psB, psB + kBlkRowParts + 16 * DRCVAR_MPC_MAX_HORIZON, lane, 64);
+          }
           BLK_ACC(0);
           __syncthreads();
           BLK_ACC(1);
           ric_blocked_phase2(s, H);
-          if (wave == kWaves - 1) rhs_parts<NU, kBlock>(s, H0T, n, H, psA, psB, lane, 128);
+          if (!dyn && wave == kWaves - 1) rhs_parts<NU, kBlock>(s, H0T, n, H, psA, psB, lane, 128);
           BLK_ACC(2);
           ric_blocked_phase3<NU>(s, H);
-          if (wave == kWaves - 2) rhs_parts<NU, kBlock>(s, H0T, n, H, psA, psB, 64 + lane, 128);
+          if (!dyn && wave == kWaves - 2) rhs_parts<NU, kBlock>(s, H0T, n, H, psA, psB, 64 + lane, 128);
           BLK_ACC(4);
           __syncthreads();
           for (int j = tid; j < n; j += kBlock) {
             double r = s.f[j] + parts_total<kBlock>(psA, j);
+            if (dyn) {  // + 2 R u (the dynamics form's H0 u carries 2 Gx'Q Gx u in psA)
+              const int jj = j / NU, ai = j - jj * NU;
+              double ru = 0.0;
+#pragma unroll
+              for (int c = 0; c < NU; ++c) ru += s.Rm[ai * NU + c] * s.u[jj * NU + c];
+              r += 2.0 * ru;
+            }
             if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
             s.rdu[j] = r;
             rdm = fmax(rdm, fabs(r));
@@ -2500,7 +2589,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     CL_NOTE(s.Ri[0]);  // the factorisation (its first pivot's inverse)
     MPC_PHASE(3);
-    if constexpr (kBlockedCode && NX == 4 && kWaves == 8) {
+    if constexpr (kBlockedSolve && NX == 4 && kWaves == 8) {
       if (blocked) solve_blocks_prepare(s, H);  // (read behind the solve's first barrier)
     }
     newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa, nullptr, blocked);  // direction, positions
@@ -2843,7 +2932,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       }
       MPC_PHASE(10);
       if (!riccati_factor_any<NU, NX, kWaves>(s, H) && !riccati_factor<NU, NX, true>(s, H)) break;
-      if constexpr (kBlockedCode && NX == 4 && kWaves == 8) {
+      if constexpr (kBlockedSolve && NX == 4 && kWaves == 8) {
         if (blocked) solve_blocks_prepare(s, H);
       }
       CL_NOTE(s.Ri[0]);
