@@ -1639,7 +1639,8 @@ __device__ inline void chain_fwd_blocked(const Lds& s, int H, double* W, const d
 // be null: 0) — read off the forward pass's states instead of a separate Mp convolution.
 template <int NU, int kBlock>
 __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c,
-                                         bool blk) {
+                                         bool blk_form) {
+  const bool blk = kBlockedSolve && kBlock == 512 && blk_form;  // the blocked chains (opt-in build)
   const int t = threadIdx.x;
   double* W = s.SV;   // [H + 1][4]: Kg_k' b_k, then p_k (backward pass), then x_k (forward pass)
   double* G = s.red;  // [H][4]: B kff_k

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4q; mkdir -p $OUT
 V=scripts/micro/variants
 S="30,3,1 30,3,1024 20,10,3 50,256,1 50,256,3"
-for v in dyn; do
+for v in dyn p; do
   echo "== mpc tests on mpc_$v"
   DRCVAR_DIAG_LIB=$V/mpc_$v.so timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_mpc.py tests/test_mpc_cluster.py > $OUT/tests_$v.log 2>&1; rc=$?
