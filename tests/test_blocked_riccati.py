@@ -212,3 +212,29 @@ def test_blocked_factorisation_and_solve_match_sequential(H, scale, seed):
     assert np.abs(du_seq.reshape(-1) - du_dense).max() <= 1e-8 * ref
     assert np.abs(du_blk.reshape(-1) - du_dense).max() <= 1e-8 * ref
     assert np.abs(du_blk - du_seq).max() <= 1e-9 * ref
+
+
+def test_h0u_through_the_dynamics_matches_the_blob():
+    """The DRCVAR_BLOCKED_DYN rows form H0 u as 2 (Gx' Q (Gx u) + R u) from an A^i B table — two
+    convolutions instead of the condensed n x n H0 that drcvar_mpc_model_init stores in the blob.
+    Same numbers (to rounding) as the blob's H0 times u, for the reference's double integrator."""
+    from tests.test_mpc import model_init
+    H = 50
+    Q, R = 2 * np.eye(4), np.eye(2)
+    rc, m, blob = model_init(A, B, C, Q, R, H)
+    assert rc == 0
+    n = 2 * H
+    H0 = blob[:n * n].reshape(n, n)
+    u = np.random.default_rng(5).normal(size=n)
+    AB = [np.linalg.matrix_power(A, i) @ B for i in range(H)]  # the kernel's s.xs table
+    X = np.zeros((H, 4))  # states x_{k+1} = sum_{j<=k} A^{k-j} B u_j (Gx u)
+    for k in range(H):
+        for j in range(k + 1):
+            X[k] += AB[k - j] @ u[2 * j:2 * j + 2]
+    Z = X @ Q.T  # Q x_{k+1}
+    h0u = np.zeros(n)
+    for j in range(H):
+        for k in range(j, H):
+            h0u[2 * j:2 * j + 2] += AB[k - j].T @ Z[k]
+        h0u[2 * j:2 * j + 2] += R @ u[2 * j:2 * j + 2]
+    np.testing.assert_allclose(2 * h0u, H0 @ u, rtol=1e-12, atol=1e-12 * np.abs(H0 @ u).max())
