@@ -29,6 +29,7 @@
 // No MFMA: ~10 flops per 16-B sample — the kernel is bounded by HBM.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 
@@ -792,78 +793,6 @@ __device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, d
   }
 }
 
-#ifdef DRCVAR_DIAG_BITONIC
-// Diagnostic build (round 4): the price of the first half of a single-barrier
-// selection — each wave sorting its own 64 P projections in registers (bitonic network over the
-// element index e = 64 r + lane: partners in other registers for strides >= 64, otherwise lane
-// xor j through quad DPP (1, 2), ds_swizzle (4), row_ror:8 (8), permlane16/32_swap (16, 32); the
-// P registers of a stage are interleaved so their chains fill each other's hazard slots).  The
-// rest of the kernel is unchanged (it reads d[] as a multiset), so the stamps' phase 2 grows by
-// exactly the sort.
-template <int J>
-__device__ __forceinline__ double lane_xor_f64(double v) {
-  if constexpr (J == 1) {
-    return dpp_f64<kDppQuadXor1>(v);
-  } else if constexpr (J == 2) {
-    return dpp_f64<kDppQuadXor2>(v);
-  } else if constexpr (J == 4) {
-    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x1F | (4 << 10));
-    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x1F | (4 << 10));
-    return __hiloint2double(hi, lo);
-  } else {
-    static_assert(J == 8);
-    return dpp_f64<0x128>(v);  // row_ror:8 = lane xor 8 within a row of 16
-  }
-}
-template <int P, int K, int J>
-__device__ __forceinline__ void bitonic_stage(double (&v)[P], int lane) {
-  if constexpr (J >= kWave) {
-    constexpr int JR = J / kWave;
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-      if ((r & JR) == 0) {
-        const bool up = ((r * kWave) & K) == 0;  // K >= 2 J >= 128: a bit of r, uniform
-        const double lo = fmin(v[r], v[r | JR]), hi = fmax(v[r], v[r | JR]);
-        v[r] = up ? lo : hi;
-        v[r | JR] = up ? hi : lo;
-      }
-    }
-  } else {
-    double a[P], b[P];
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-      if constexpr (J == 16 || J == 32) {  // {v, partner} = the swap's two results
-        const auto lo = J == 16 ? __builtin_amdgcn_permlane16_swap(__double2loint(v[r]), __double2loint(v[r]), false, false)
-                                : __builtin_amdgcn_permlane32_swap(__double2loint(v[r]), __double2loint(v[r]), false, false);
-        const auto hi = J == 16 ? __builtin_amdgcn_permlane16_swap(__double2hiint(v[r]), __double2hiint(v[r]), false, false)
-                                : __builtin_amdgcn_permlane32_swap(__double2hiint(v[r]), __double2hiint(v[r]), false, false);
-        a[r] = __hiloint2double(hi[0], lo[0]);
-        b[r] = __hiloint2double(hi[1], lo[1]);
-      } else {
-        a[r] = v[r];
-        b[r] = lane_xor_f64<J>(v[r]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-      const int e = r * kWave + lane;
-      const bool keep_min = (((e & K) == 0) == ((e & J) == 0));
-      v[r] = keep_min ? fmin(a[r], b[r]) : fmax(a[r], b[r]);
-    }
-  }
-}
-template <int P, int K, int J>
-__device__ __forceinline__ void bitonic_merge(double (&v)[P], int lane) {
-  bitonic_stage<P, K, J>(v, lane);
-  if constexpr (J > 1) bitonic_merge<P, K, J / 2>(v, lane);
-}
-template <int P, int K = 2>
-__device__ __forceinline__ void wave_bitonic_sort(double (&v)[P], int lane) {
-  static_assert((P & (P - 1)) == 0, "power-of-two registers");
-  bitonic_merge<P, K, K / 2>(v, lane);
-  if constexpr (K < P * kWave) wave_bitonic_sort<P, 2 * K>(v, lane);
-}
-#endif
 
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
@@ -884,20 +813,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
                       GenArgs gen) {
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << LOG_NB;
-  // window lists (small plans, -DDRCVAR_WINLIST): every in-window sample is kept in its wave's
-  // LDS list during the window pass, so after barrier 2 wave 0 finishes alone (no candidate pass,
-  // no barrier 3).  MEASURED AND NOT KEPT (round 3): C3 4.73 -> 6.05 us per step (HIP events) —
-  // wave 0's serial pass over ~300 window values (a ballot compaction per slot) is longer than
-  // the parallel candidate pass + barrier 3 it replaces.
-#ifdef DRCVAR_WINLIST
-  constexpr bool kList = P <= 8;
-#else
-  constexpr bool kList = false;
-#endif
   __shared__ uint32_t hist[hist_words<NB>()];
   __shared__ double cand[NW * kCap];
-  __shared__ double win[kList ? NW * P * kWave : 1];
-  __shared__ double lane_tail[(kList || P <= 8) ? BLOCK : 1];
+  __shared__ double lane_tail[P <= 8 ? BLOCK : 1];
   __shared__ uint32_t wcount[NW];
   __shared__ uint32_t wbelow_sh[NW];
   // Small plans (the latency-bound ones) place the histogram window from a 64-sample pilot after
@@ -984,10 +902,13 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 #pragma unroll
       for (int j = 0; j < P; ++j) {
         const int i = tid + j * BLOCK;
-        if (i >= pairs) {
-          const dbl2 v = gen_stage[(i < n ? i : n - 1) - pairs];
+        if (i >= pairs && i < n) {
+          const dbl2 v = gen_stage[i - pairs];
           x[j] = v.x;
           y[j] = v.y;
+        } else if (i >= n) {  // idle slot (masked by every sum): the nominal point, no LDS read
+          x[j] = gnx;
+          y[j] = gny;
         }
       }
     }
@@ -1110,9 +1031,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
 #pragma unroll
   for (int j = 0; j < P; ++j)  // +inf padding: never below, inside or a candidate
     d[j] = (tid + j * BLOCK < n) ? project(h0, h1, x[j], y[j]) : INFINITY;
-#ifdef DRCVAR_DIAG_BITONIC
-  if constexpr ((P & (P - 1)) == 0) wave_bitonic_sort<P>(d, lane);
-#endif
   const double mu_d = h0 * mux + h1 * muy;
   double var_d;
   if constexpr (kPilot) {  // variance of the pilot's projections about the exact mean, in fp32
@@ -1148,8 +1066,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   double sq = 0.0;  // sum over samples below the target bucket of (d - mu_d)
   if (fast) {
     uint32_t wbelow = 0;  // samples of this wave below the window (wave-uniform)
-    uint32_t wlist = 0;   // samples of this wave in the window (list length, wave-uniform)
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
 #pragma unroll
     for (int j = 0; j < P; ++j) {
       const double v = d[j];
@@ -1160,17 +1076,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       const bool inw = !low && tv < kNB;
       const int b = inw ? static_cast<int>(tv) : 0;  // 0 <= b <= NB - 1 inside the window
       if (inw) atomicAdd(&hist[hist_slot<NB>(b)], 1u);
-      if constexpr (kList) {
-        append_candidate(win + wave * (P * kWave), wlist, inw, v, lt_mask);
-      } else {
-        const uint32_t cj = inw ? static_cast<uint32_t>(b) : 0xFFFFu;
-        if (j % 2 == 0) code[j / 2] = cj;
-        else code[j / 2] |= cj << 16;
-      }
-    }
-    if constexpr (kList) {
-      lane_tail[tid] = sq;  // below-window partial sums, combined by wave 0 in a fixed order
-      if (lane == 0) wcount[wave] = wlist;
+      const uint32_t cj = inw ? static_cast<uint32_t>(b) : 0xFFFFu;
+      if (j % 2 == 0) code[j / 2] = cj;
+      else code[j / 2] |= cj << 16;
     }
     if (lane == 0) wbelow_sh[wave] = wbelow;
     DRCVAR_STAMP(3);
@@ -1204,43 +1112,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // ---- 4. candidates of the target bucket + tail sum below them -----------------------------
   double tau, dsum;  // dsum = sum_{d<tau} (d - tau)
   double rch;        // R_c |h| (risk_metrics.py:293, :234), wave 0
-  if (kList && fast) [[likely]] {
-    // wave 0 alone: the target bucket's candidates and the in-window part of the tail sum come
-    // from the waves' window lists (each value re-binned by the same fma as in the window pass,
-    // so the classification is identical); the order of every sum is fixed
-    if (wave != 0) {
-      if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
-      return;
-    }
-    DRCVAR_STAMP(5);
-    const uint32_t ubin = static_cast<uint32_t>(bin);
-    double tail = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) tail += lane_tail[w * kWave + lane];
-    uint32_t ccount = 0;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const uint32_t nw = wcount[w];
-#pragma unroll
-      for (int r = 0; r < P; ++r) {
-        const uint32_t idx = static_cast<uint32_t>(r * kWave + lane);
-        const bool in = idx < nw;
-        const double v = in ? win[w * (P * kWave) + idx] : 0.0;
-        const uint32_t b = static_cast<uint32_t>(map(v));  // in-window values: 0 <= b < NB
-        tail += (in && b < ubin) ? v - mu_d : 0.0;
-        append_candidate(cand, ccount, in && b == ubin, v, lt_mask);
-      }
-    }
-    const double s_below = wave_reduce<OpAdd>(tail);
-    rch = prm.rc * norm_h(h0, h1);  // R_c |h|
-    if (lane == 0) wcount[0] = ccount;  // the candidates as one region (wave-local hand-off)
-    wave_lds_fence();
-    double s_cand;
-    tau = rank_candidates<1>(cand, wave_counts<1>(wcount, lane), c, rr, lane, &s_cand);
-    dsum = (s_below - static_cast<double>(rank - rr) * (tau - mu_d)) + s_cand;
-    DRCVAR_STAMP(6);
-  } else if (fast) [[likely]] {
+  if (fast) [[likely]] {
     uint32_t wbase = 0;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const uint32_t ubin = static_cast<uint32_t>(bin);
@@ -1303,11 +1175,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       double lo[1] = {INFINITY}, hi[1] = {-INFINITY};
 #pragma unroll
       for (int j = 0; j < P; ++j) {
-#ifdef DRCVAR_DIAG_BITONIC
-        if (d[j] != INFINITY) {  // sorted: the padding sits at the end of the wave's order
-#else
         if (tid + j * BLOCK < n) {
-#endif
           lo[0] = fmin(lo[0], d[j]);
           hi[0] = fmax(hi[0], d[j]);
         }
@@ -1484,20 +1352,25 @@ struct Launch {
 // grid (n_steps, obstacles), at most kMaxGridY obstacles per launch (the y-dimension limit):
 // larger batches are split into obstacle chunks on the host
 constexpr int64_t kMaxGridY = 65535;
+constexpr int kMaxDevices = 64;  // per-device state of the launcher (the dynamic-LDS attribute)
 
 template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
-void launch_form(const Launch& L) {
+int launch_form(const Launch& L) {
   const int64_t n_obs = L.units / L.n_steps;
   size_t dyn = DRCVAR_HS_LDS_PAD;
   if constexpr (LOAD == kLoadGen && BLOCK * P <= kPairMax) {
     // the paired draws' staging: [pairs] of 16 B (80 KB at N = 10 000: above the default 64 KB
-    // limit of dynamic LDS, raised once per kernel)
+    // limit of dynamic LDS, raised once per kernel and device; a failure is a launch error)
     dyn = static_cast<size_t>(L.gen.pairs) * 16;
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kPairMax / 2 * 16));
-      attr_set = true;
+    static std::atomic<bool> attr_set[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return DRCVAR_ERR_LAUNCH;
+    if (!attr_set[dev].load(std::memory_order_acquire)) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(kPairMax / 2 * 16)) != hipSuccess)
+        return DRCVAR_ERR_LAUNCH;
+      attr_set[dev].store(true, std::memory_order_release);
     }
   }
   for (int64_t o0 = 0; o0 < n_obs; o0 += kMaxGridY) {
@@ -1510,10 +1383,11 @@ void launch_form(const Launch& L) {
                        L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH,
                        L.status ? L.status + o0 * L.n_steps : nullptr, L.gen);
   }
+  return DRCVAR_OK;
 }
 
 template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
-void launch_plan(Launch L, bool vec) {
+int launch_plan(Launch L, bool vec) {
   const int64_t sub = P <= 8 ? kWave : BLOCK;  // the window's subsample: pilot or row 0 (kernel)
   L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < sub ? L.n : sub);
   L.prm.hist_scale = static_cast<double>(1 << LOG_NB) / (2.0 * L.prm.window_sd);
@@ -1521,18 +1395,11 @@ void launch_plan(Launch L, bool vec) {
   // cache-resident across steps) they cost 3 %, so only launches larger than the MALL use them
   const bool nt = vec && L.units * L.n * 16 > kNtBytes;
   if constexpr (!GIVEN_H) {
-    if (L.generate) {
-      launch_form<BLOCK, P, LOG_NB, kLoadGen, false>(L);
-      return;
-    }
+    if (L.generate) return launch_form<BLOCK, P, LOG_NB, kLoadGen, false>(L);
   }
-  if (nt) {
-    launch_form<BLOCK, P, LOG_NB, kLoadNt, GIVEN_H>(L);
-  } else if (vec) {
-    launch_form<BLOCK, P, LOG_NB, kLoadVec, GIVEN_H>(L);
-  } else {
-    launch_form<BLOCK, P, LOG_NB, kLoadPair, GIVEN_H>(L);
-  }
+  if (nt) return launch_form<BLOCK, P, LOG_NB, kLoadNt, GIVEN_H>(L);
+  if (vec) return launch_form<BLOCK, P, LOG_NB, kLoadVec, GIVEN_H>(L);
+  return launch_form<BLOCK, P, LOG_NB, kLoadPair, GIVEN_H>(L);
 }
 
 template <bool GIVEN_H>
@@ -1564,22 +1431,24 @@ int dispatch(const Launch& L, int threads, int per) {
   const int p = pick_plan(L.n, threads, per);
   if (p < 0) return DRCVAR_ERR_UNSUPPORTED;
   (void)hipGetLastError();  // clear stale errors from unrelated work
+  int rc = DRCVAR_OK;
   switch (p) {
-    case 0: launch_plan<64, 2, 7, GIVEN_H>(L, vec); break;
-    case 1: launch_plan<128, 4, 8, GIVEN_H>(L, vec); break;
-    case 2: launch_plan<256, 4, 9, GIVEN_H>(L, vec); break;
-    case 3: launch_plan<256, 8, 10, GIVEN_H>(L, vec); break;
-    case 4: launch_plan<256, 16, 10, GIVEN_H>(L, vec); break;
-    case 5: launch_plan<256, 20, 10, GIVEN_H>(L, vec); break;
-    case 6: launch_plan<512, 16, 10, GIVEN_H>(L, vec); break;
-    case 7: launch_plan<512, 20, 10, GIVEN_H>(L, vec); break;
-    case 8: launch_plan<1024, 12, 10, GIVEN_H>(L, vec); break;
-    case 9: launch_plan<1024, 16, 10, GIVEN_H>(L, vec); break;
-    case 10: launch_plan<64, 16, 9, GIVEN_H>(L, vec); break;
-    case 11: launch_plan<128, 8, 9, GIVEN_H>(L, vec); break;
-    case 12: launch_plan<512, 2, 9, GIVEN_H>(L, vec); break;
-    default: launch_plan<1024, 10, 10, GIVEN_H>(L, vec); break;
+    case 0: rc = launch_plan<64, 2, 7, GIVEN_H>(L, vec); break;
+    case 1: rc = launch_plan<128, 4, 8, GIVEN_H>(L, vec); break;
+    case 2: rc = launch_plan<256, 4, 9, GIVEN_H>(L, vec); break;
+    case 3: rc = launch_plan<256, 8, 10, GIVEN_H>(L, vec); break;
+    case 4: rc = launch_plan<256, 16, 10, GIVEN_H>(L, vec); break;
+    case 5: rc = launch_plan<256, 20, 10, GIVEN_H>(L, vec); break;
+    case 6: rc = launch_plan<512, 16, 10, GIVEN_H>(L, vec); break;
+    case 7: rc = launch_plan<512, 20, 10, GIVEN_H>(L, vec); break;
+    case 8: rc = launch_plan<1024, 12, 10, GIVEN_H>(L, vec); break;
+    case 9: rc = launch_plan<1024, 16, 10, GIVEN_H>(L, vec); break;
+    case 10: rc = launch_plan<64, 16, 9, GIVEN_H>(L, vec); break;
+    case 11: rc = launch_plan<128, 8, 9, GIVEN_H>(L, vec); break;
+    case 12: rc = launch_plan<512, 2, 9, GIVEN_H>(L, vec); break;
+    default: rc = launch_plan<1024, 10, 10, GIVEN_H>(L, vec); break;
   }
+  if (rc != DRCVAR_OK) return rc;
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
 }
 

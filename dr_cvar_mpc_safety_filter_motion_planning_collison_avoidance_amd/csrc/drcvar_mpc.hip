@@ -59,7 +59,7 @@
 namespace drcvar_mpc_detail {
 
 struct BlobLayout {
-  int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, UF1, UF2, UFOK, H0T, total;
+  int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, UF1, UF2, UFOK, total;
 };
 
 inline BlobLayout blob_layout(int nx, int nu, int H) {
@@ -81,9 +81,6 @@ inline BlobLayout blob_layout(int nx, int nu, int H) {
   L.UF1 = o; o += n * nx;
   L.UF2 = o; o += n * H * nx;
   L.UFOK = o; o += 1;
-  // H0 transposed (bitwise): the affine-rhs rows read column j of it, so the lanes (consecutive
-  // rows j) read consecutive doubles
-  L.H0T = o; o += n * n;
   L.total = o;
   return L;
 }
@@ -170,10 +167,8 @@ constexpr int kClusterMaxProblems = 8;
 constexpr int kClusterMinObstacles = 64;
 constexpr int kClusterObstaclesPerGroup = 16;  // C5: 16 workgroups (8..32 measured within 4 %)
 constexpr int kClusterMax = 32;
-#ifndef DRCVAR_CLUSTER_BLOCK
-#define DRCVAR_CLUSTER_BLOCK 512
-#endif
-constexpr int kClusterBlock = DRCVAR_CLUSTER_BLOCK;  // threads per workgroup of the clustered form
+// threads per workgroup of the clustered form (256 measured 3-7 % slower at every shape)
+constexpr int kClusterBlock = 512;
 constexpr int kClusterCUs = 256;  // workspace sizing; launches use the device's own CU count
 constexpr int kRec = 512;                        // doubles per exchange record
 constexpr int kRecScalars = kPerStepQ * 64;      // [kPerStepQ][64] per-step sums, then scalars
@@ -194,7 +189,6 @@ enum { kSiteStart = 1, kSiteP1, kSiteP23, kSiteP4, kSitePolishHess, kSitePolishR
 constexpr int kStampProblems = 64, kStampSlots = 20;
 __device__ unsigned long long g_mpc_stamps[kStampProblems * kStampSlots];
 __device__ unsigned long long g_cl_stamps[8];  // cluster exchange sub-phases, problem 0, group 0
-__device__ unsigned long long g_blk_stamps[64];  // blocked factorisation: [wave][phase], group 0
 #define CL_STAMP(k)                                                     \
   do {                                                                  \
     if (threadIdx.x == 0 && blockIdx.x == 0) {                          \
@@ -859,455 +853,6 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
   return riccati_factor_finish<NU, NX>(s, H);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Blocked factorisation (round 4; 8-wave workgroups, NX = 4, H >= kBlkMinH).  The recursion above
-// is a chain of H dependent steps on one wave (~0.9 k cycles each: ~46 k per factorisation at
-// H = 50).  Here the horizon is cut into W = 8 blocks [k_w, k_{w+1}), one per wave:
-//   phase 1  waves 1..W-1 at once.  The last block runs the ordinary recursion from the true P_H
-//            (its gains are final).  Every other block w runs it from the zero terminal (J = 0) and
-//            carries the block's element E_w = (J_E, A_E, C_E): for every terminal P_e,
-//              P_{k_w} = J_E + A_E' (I + P_e C_E)^-1 P_e A_E
-//            (lanes 0-15: J_E entries; 16-31: A_E <- A_E (A - B Kg); 32-47: C_E <- C_E + G Re^-1 G',
-//            G = A_E B with the old A_E — the LQ value-function element of Sarkka & Garcia-
-//            Fernandez, built step by step beside the recursion it summarises).
-//   phase 2  one wave: the true P at every block end from the back, P_{k_w} = E_w(P_{k_{w+1}}),
-//            w = W-2 .. 1 (a 4 x 4 solve without pivoting per block; scripts/micro/
-//            riccati_block_lab.py: relative pivots >= 3e-3 on every captured Newton system).
-//   phase 3  waves 0..W-2 at once: the ordinary recursion of each block from its true end value,
-//            writing the gains.
-// Chain: ~7 + 6 + 7 short steps at H = 50 instead of 50.  Scratch: kBlkSlot doubles of s.red per
-// wave (free from the end of P1 to the solve).  Results differ from the sequential recursion by
-// rounding only; every workgroup of a cluster runs the same code (the same bits).  A failed pivot
-// anywhere sets the wave's flag; the caller then repeats the sequential form.
-// The lane and wave indices as fresh values at each call: the blocked phases are inlined into
-// the interior-point loop, and without this the compiler hoisted their lane-dependent LDS
-// addresses out of it (dozens of VGPRs live across the whole loop: 1 KB of scratch per lane)
-__device__ __forceinline__ int opaque_lane() {
-  int lane = static_cast<int>(threadIdx.x & 63);
-  asm volatile("" : "+v"(lane));
-  return lane;
-}
-__device__ __forceinline__ int opaque_wave() {
-  int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  asm volatile("" : "+s"(w));
-  return w;
-}
-// per wave: J @0, T @16, U @32, A_E @48, C_E @64 (phase 1), P_e @80, flags @96 / @97, and phase
-// 3's J, T, U @112 (so that a block's element stays intact while its phase 3 runs)
-constexpr int kBlkSlot = 160;
-constexpr int kBlkMinH = 16;
-#ifdef DRCVAR_BLOCKED
-constexpr bool kBlockedCode = true;  // the blocked factorisation (A/B builds)
-#else
-constexpr bool kBlockedCode = false;
-#endif
-#ifdef DRCVAR_BLOCKED_SOLVE
-constexpr bool kBlockedSolve = kBlockedCode;  // ... and the blocked solve chains (measured slower)
-#else
-constexpr bool kBlockedSolve = false;
-#endif
-#ifdef DRCVAR_BLOCKED_DYN
-constexpr bool kBlockedDyn = kBlockedCode && !kBlockedSolve;  // rows' H0 u through the dynamics
-#else
-constexpr bool kBlockedDyn = false;
-#endif
-#ifndef DRCVAR_BLK_W
-#define DRCVAR_BLK_W 8
-#endif
-constexpr int kBlkW = DRCVAR_BLK_W;  // blocks (waves 0..kBlkW-1 of an 8-wave workgroup)
-static_assert(kBlkW >= 3 && kBlkW <= 8, "blocked factorisation: 3..8 blocks");
-constexpr int kBlkRowParts = 4 * 128;  // partial sums of the rows (rhs_parts): n * PARTS <= 480
-static_assert(kBlkW * kBlkSlot + 2 * kBlkRowParts + 20 * DRCVAR_MPC_MAX_HORIZON <= 8 * kPerStepQ * 64,
-              "blocked factorisation scratch exceeds s.red");
-
-__device__ __forceinline__ int blk_begin(int w, int H) { return (w * H) / kBlkW; }
-
-// The rows of r_du = H0 u + f + Gp' v (+ box) and dua = -r_du - rU - Gp' za as PARTS partial sums
-// each, over threads t, t + nt, ... (part-major: consecutive lanes take consecutive rows, so the
-// loads of H0T coalesce): psA[j * PARTS + part] = part of (Gp' v + H0 u)[j], psB[...] = part of
-// (Gp' za)[j], in gpt_row's order (its acc[part]); parts_total combines them in its order.
-template <int NU, int kBlock>
-__device__ inline void rhs_parts(const Lds& s, const double* H0T, int n, int H, double* psA, double* psB,
-                                 int t, int nt) {
-  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
-  for (int e = t; e < n * PARTS; e += nt) {
-    const int part = e / n, j_a = e - part * n;
-    const int j = j_a / NU, a = j_a - j * NU;
-    double acc = 0.0, acc2 = 0.0;
-    for (int k = j + part; k < H; k += PARTS) {
-      const double* m = s.Mp + (k - j) * 2 * NU;
-      acc += m[a] * s.v[2 * k] + m[NU + a] * s.v[2 * k + 1];
-      acc2 += m[a] * s.za[2 * k] + m[NU + a] * s.za[2 * k + 1];
-    }
-    for (int l0 = part; l0 < n; l0 += 8 * PARTS) {  // eight H0 loads in flight
-      double hv[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int l = l0 + q * PARTS;
-        hv[q] = l < n ? H0T[static_cast<int64_t>(l) * n + j_a] : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (l0 + q * PARTS < n) acc += hv[q] * s.u[l0 + q * PARTS];
-    }
-    psA[j_a * PARTS + part] = acc;
-    psB[j_a * PARTS + part] = acc2;
-  }
-}
-
-// rhs_parts with the H0 u term through the dynamics: psA's part holds (Gp' v) + 2 (Gx' Z) over
-// its k (Z = Q Gx u per step, [H][4], AB[i] = A^i B in s.xs), psB (Gp' za) as rhs_parts.
-template <int NU, int kBlock>
-__device__ inline void rhs_parts_dyn(const Lds& s, int n, int H, double* psA, double* psB,
-                                     const double* Zs, int t, int nt) {
-  constexpr int PARTS = kBlock >= 512 ? 4 : 2;
-  for (int e = t; e < n * PARTS; e += nt) {
-    const int part = e / n, j_a = e - part * n;
-    const int j = j_a / NU, a = j_a - j * NU;
-    double acc = 0.0, acc2 = 0.0, accz = 0.0;
-    for (int k = j + part; k < H; k += PARTS) {
-      const double* m = s.Mp + (k - j) * 2 * NU;
-      acc += m[a] * s.v[2 * k] + m[NU + a] * s.v[2 * k + 1];
-      acc2 += m[a] * s.za[2 * k] + m[NU + a] * s.za[2 * k + 1];
-      const double* ab = s.xs + (k - j) * 4 * NU + a;
-      accz += (ab[0] * Zs[4 * k] + ab[NU] * Zs[4 * k + 1]) + (ab[2 * NU] * Zs[4 * k + 2] + ab[3 * NU] * Zs[4 * k + 3]);
-    }
-    psA[j_a * PARTS + part] = acc + 2.0 * accz;
-    psB[j_a * PARTS + part] = acc2;
-  }
-}
-
-// Steps ke-1 .. kb of the recursion on the calling wave, from J (the wave's slot, 4 x 4 row-major).
-// kElem: also the element's A_E / C_E (lanes 16-47); gains: write Kg_k, Ri_k.  False on a failed
-// pivot (the steps stop there).
-template <int NU, bool kElem>
-__device__ __forceinline__ bool ric_block_steps(const Lds& s, int H, double* sl, int kb, int ke, bool gains) {
-  const int lane = opaque_lane();
-  const int g = lane >> 4, e = lane & 15, i = e >> 2, j = e & 3;
-  double* J = sl;
-  double* T = sl + 16;
-  double* U = sl + 32;
-  double* AE = sl + 48;
-  double* CE = sl + 64;
-  const int uc = j < NU ? j : 0;
-  double Acol[4], Bcol[4], ai[4], Bm[4][NU], R2[NU][NU];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    Acol[m] = s.Am[m * kMx + j];
-    Bcol[m] = s.Bm[m * NU + uc];
-    ai[m] = s.Am[m * kMx + i];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) Bm[m][c] = s.Bm[m * NU + c];
-  }
-#pragma unroll
-  for (int c = 0; c < NU; ++c)
-#pragma unroll
-    for (int d = 0; d < NU; ++d) R2[c][d] = 2.0 * s.Rm[c * NU + d];
-  const double c0i = s.Cm[i], c1i = s.Cm[kMx + i], c0j = s.Cm[j], c1j = s.Cm[kMx + j];
-  const double q2 = 2.0 * s.Qm[i * kMx + j];
-  auto qb = [&](int k) {  // Qb_{k+1}, entry (i, j)
-    const double S00 = s.S[k], S01 = s.S[H + k], S11 = s.S[2 * H + k];
-    return q2 + c0i * (S00 * c0j + S01 * c1j) + c1i * (S01 * c0j + S11 * c1j);
-  };
-  bool ok = true;
-  for (int k = ke - 1; k >= kb && ok; --k) {
-    wave_lds_fence();
-    // (a) T = J A, U = J B (lanes 0-15); the element lanes load the old A_E rows they need
-    double prow[4], ari[4], arj[4], ce_old = 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) prow[m] = J[i * 4 + m];
-    if constexpr (kElem) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        ari[m] = AE[i * 4 + m];
-        arj[m] = AE[j * 4 + m];
-      }
-      ce_old = CE[e];
-    }
-    {
-      double t = 0.0, uu = 0.0;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        t += prow[m] * Acol[m];
-        uu += prow[m] * Bcol[m];
-      }
-      if (g == 0) {
-        T[e] = t;
-        if (j < NU) U[i * NU + j] = uu;
-      }
-    }
-    wave_lds_fence();
-    // (b) Re = Rb + B'U and its inverse (every lane), L = B'T, Kg column j
-    double ti[4], tj[4], Um[4][NU], du[NU];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      ti[m] = T[m * 4 + i];
-      tj[m] = T[m * 4 + j];
-#pragma unroll
-      for (int c = 0; c < NU; ++c) Um[m][c] = U[m * NU + c];
-    }
-#pragma unroll
-    for (int c = 0; c < NU; ++c) du[c] = s.DU[k * NU + c];
-    const double qnext = k > 0 ? qb(k - 1) : 0.0;
-    double Re[NU][NU], Ri[NU][NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c)
-#pragma unroll
-      for (int d = 0; d < NU; ++d) {
-        double acc = R2[c][d] + (c == d ? du[c] : 0.0);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc += Bm[m][c] * Um[m][d];
-        Re[c][d] = acc;
-      }
-    ok = spd_inverse<NU>(Re, Ri);
-    double Li[NU], Lj[NU], Kj[NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      double li = 0.0, lj = 0.0;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        li += Bm[m][c] * ti[m];
-        lj += Bm[m][c] * tj[m];
-      }
-      Li[c] = li;
-      Lj[c] = lj;
-    }
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      double acc = 0.0;
-#pragma unroll
-      for (int d = 0; d < NU; ++d) acc += Ri[c][d] * Lj[d];
-      Kj[c] = acc;
-    }
-    if (gains) {
-      if (g == 0 && i == j) {
-#pragma unroll
-        for (int c = 0; c < NU; ++c) s.Kg[(k * NU + c) * 4 + j] = Kj[c];
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int c = 0; c < NU; ++c)
-#pragma unroll
-          for (int d = 0; d < NU; ++d) s.Ri[(k * NU + c) * NU + d] = Ri[c][d];
-      }
-    }
-    if (g == 0 && k > 0 && i >= j) {  // J <- Qb_k + A'J A - L'Kg (lower triangle, mirrored)
-      double acc = qnext;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc += ai[m] * tj[m];
-#pragma unroll
-      for (int c = 0; c < NU; ++c) acc -= Li[c] * Kj[c];
-      J[i * 4 + j] = acc;
-      J[j * 4 + i] = acc;
-    }
-    if constexpr (kElem) {
-      if (g == 1) {  // A_E <- A_E (A - B Kg): entry (i, j) from column j of the closed loop
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          double f = Acol[m];
-#pragma unroll
-          for (int c = 0; c < NU; ++c) f -= Bm[m][c] * Kj[c];
-          acc += ari[m] * f;
-        }
-        AE[e] = acc;
-      } else if (g == 2) {  // C_E <- C_E + G Re^-1 G', G = A_E B (old A_E)
-        double gi[NU], gj[NU];
-#pragma unroll
-        for (int c = 0; c < NU; ++c) {
-          double x = 0.0, y = 0.0;
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            x += ari[m] * Bm[m][c];
-            y += arj[m] * Bm[m][c];
-          }
-          gi[c] = x;
-          gj[c] = y;
-        }
-        double acc = ce_old;
-#pragma unroll
-        for (int c = 0; c < NU; ++c) {
-          double r = 0.0;
-#pragma unroll
-          for (int d = 0; d < NU; ++d) r += Ri[c][d] * gj[d];
-          acc += gi[c] * r;
-        }
-        CE[e] = acc;
-      }
-    }
-  }
-  wave_lds_fence();
-  return ok;
-}
-
-// Phase 1 (waves 1..W-1; wave 0 returns at once and is free for other work).
-template <int NU>
-__device__ __forceinline__ void ric_blocked_phase1(const Lds& s, int H) {
-  const int lane = opaque_lane(), w = opaque_wave();
-  if (w >= kBlkW) return;
-  double* sl = s.red + w * kBlkSlot;
-  if (lane == 0) reinterpret_cast<int*>(sl)[2 * 97] = 0;  // P_e not yet published (phase 2)
-  if (w == 0) {
-    if (lane == 0) sl[96] = 0.0;
-    return;
-  }
-  const int e = lane & 15, i = e >> 2, j = e & 3;
-  const bool last = w == kBlkW - 1;
-  if (lane < 16) {
-    double v = 0.0;
-    if (last) {  // J = Qb_H
-      const double S00 = s.S[H - 1], S01 = s.S[2 * H - 1], S11 = s.S[3 * H - 1];
-      const double c0i = s.Cm[i], c1i = s.Cm[kMx + i], c0j = s.Cm[j], c1j = s.Cm[kMx + j];
-      v = 2.0 * s.Qm[i * kMx + j] + c0i * (S00 * c0j + S01 * c1j) + c1i * (S01 * c0j + S11 * c1j);
-    }
-    sl[e] = v;
-    sl[48 + e] = i == j ? 1.0 : 0.0;  // A_E = I
-    sl[64 + e] = 0.0;                 // C_E = 0
-  }
-  const int kb = blk_begin(w, H), ke = blk_begin(w + 1, H);
-  const bool ok = last ? ric_block_steps<NU, false>(s, H, sl, kb, ke, true)
-                       : ric_block_steps<NU, true>(s, H, sl, kb, ke, false);
-  if (lane == 0) sl[96] = ok ? 0.0 : 1.0;
-}
-
-// Phase 2 (wave 0): P at every block end, from the back.  P_e of block w lands in slot w @80
-// (block W-2 reads the last block's J directly).
-__device__ __forceinline__ void ric_blocked_phase2(const Lds& s, int H) {
-  (void)H;
-  if (threadIdx.x >= 64) return;
-  const int lane = opaque_lane(), e = lane & 15, i = e >> 2, j = e & 3;
-  double* sc = s.red;  // wave 0's slot: T / U areas as the solve's scratch
-  bool ok = true;
-  for (int w = kBlkW - 2; w >= 1; --w) {
-    const double* E = s.red + w * kBlkSlot;  // J_E @0, A_E @48, C_E @64
-    const double* Pe = w == kBlkW - 2 ? s.red + (kBlkW - 1) * kBlkSlot : E + 80;
-    double* out = s.red + (w - 1) * kBlkSlot + 80;
-    wave_lds_fence();
-    double prow[4], aec[4], cec[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      prow[m] = Pe[i * 4 + m];
-      aec[m] = E[48 + m * 4 + j];
-      cec[m] = E[64 + m * 4 + j];
-    }
-    double nij = i == j ? 1.0 : 0.0, mij = 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      nij += prow[m] * cec[m];
-      mij += prow[m] * aec[m];
-    }
-    if (lane < 16) {
-      sc[16 + e] = nij;  // N = I + P_e C_E
-      sc[32 + e] = mij;  // M = P_e A_E
-    }
-    wave_lds_fence();
-    // Y = N^-1 M, columns j and i (every lane its own copy of N; no pivoting)
-    double N[4][4], yj[4], yi[4], aei[4], aej[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) N[r][c] = sc[16 + r * 4 + c];
-      yj[r] = sc[32 + r * 4 + j];
-      yi[r] = sc[32 + r * 4 + i];
-      aei[r] = E[48 + r * 4 + i];
-      aej[r] = E[48 + r * 4 + j];
-    }
-    const double jij = E[i * 4 + j], jji = E[j * 4 + i];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const double piv = N[q][q];
-      ok = ok && isfinite(piv) && fabs(piv) > 1e-6;
-      const double ip = rcp(piv);
-#pragma unroll
-      for (int r = q + 1; r < 4; ++r) {
-        const double f = N[r][q] * ip;
-#pragma unroll
-        for (int c = q + 1; c < 4; ++c) N[r][c] -= f * N[q][c];
-        yj[r] -= f * yj[q];
-        yi[r] -= f * yi[q];
-      }
-      N[q][q] = ip;
-    }
-#pragma unroll
-    for (int q = 3; q >= 0; --q) {
-      double a = yj[q], b = yi[q];
-#pragma unroll
-      for (int c = q + 1; c < 4; ++c) {
-        a -= N[q][c] * yj[c];
-        b -= N[q][c] * yi[c];
-      }
-      yj[q] = a * N[q][q];
-      yi[q] = b * N[q][q];
-    }
-    double rij = jij, rji = jji;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      rij += aei[m] * yj[m];
-      rji += aej[m] * yi[m];
-    }
-    if (lane < 16) out[e] = 0.5 * (rij + rji);
-    wave_lds_fence();  // (LDS operations of one wave complete in order: the values precede the flag)
-    if (lane == 0)
-      __hip_atomic_store(reinterpret_cast<int*>(out - 80) + 2 * 97, 1, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  wave_lds_fence();
-  if (!ok && lane == 0) s.red[96] = 1.0;
-}
-
-// Phase 3 (waves 0..W-2): each block from its true end value, writing the gains.
-template <int NU>
-__device__ __forceinline__ void ric_blocked_phase3(const Lds& s, int H) {
-  const int lane = opaque_lane(), w = opaque_wave();
-  if (w >= kBlkW - 1) return;
-  double* sl = s.red + w * kBlkSlot;
-  const double* Pe = w == kBlkW - 2 ? s.red + (kBlkW - 1) * kBlkSlot : sl + 80;
-  // no barrier behind phase 2: blocks 1..W-3 start when wave 0 has published their end value
-  // (block W-2's is the last block's J, block 0's is wave 0's own)
-  if (w >= 1 && w <= kBlkW - 3) {
-    while (__hip_atomic_load(reinterpret_cast<int*>(sl) + 2 * 97, __ATOMIC_ACQUIRE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-      __builtin_amdgcn_s_sleep(1);
-  }
-  if (lane < 16) sl[112 + lane] = Pe[lane];
-  const bool ok = ric_block_steps<NU, false>(s, H, sl + 112, blk_begin(w, H), blk_begin(w + 1, H), true);
-  if (!ok && lane == 0) sl[96] = 1.0;
-}
-
-// After a barrier behind phase 3: the outcome (uniform) and the solve maps, as
-// riccati_factor_finish.
-template <int NU, int NX>
-__device__ __forceinline__ bool ric_blocked_finish(const Lds& s, int H) {
-  double bad = 0.0;
-#pragma unroll
-  for (int w = 0; w < kBlkW; ++w) bad += s.red[w * kBlkSlot + 96];
-  return riccati_maps<NU, NX>(s, H, bad == 0.0);
-}
-
-// Whether a kernel form factorises blocked (uniform).
-template <int NX, int kWaves>
-__device__ __forceinline__ bool ric_blocked_form(int H) {
-  return kBlockedCode && NX == 4 && kWaves == 8 && H >= kBlkMinH;
-}
-
-// riccati_factor with the blocked form where it applies; a failed blocked factorisation is
-// repeated sequentially.  Every thread calls it.
-template <int NU, int NX, int kWaves>
-__device__ __forceinline__ bool riccati_factor_any(const Lds& s, int H) {
-  if constexpr (kBlockedCode && NX == 4 && kWaves == 8) {
-    if (ric_blocked_form<NX, kWaves>(H)) {
-      ric_blocked_phase1<NU>(s, H);
-      __syncthreads();
-      ric_blocked_phase2(s, H);
-      ric_blocked_phase3<NU>(s, H);
-      __syncthreads();
-      if (ric_blocked_finish<NU, NX>(s, H)) return true;
-      __syncthreads();
-    }
-  }
-  return riccati_factor<NU, NX>(s, H);
-}
-
 // Solve K x = b with the factorisation above; b in x[0..n) (LDS), overwritten by the solution.
 // Vectors travel between lanes by readlane (lane m < NX holds entry m), so a step of either pass
 // has no LDS round trip on its critical path; the step's gains are loaded one step ahead.
@@ -1483,164 +1028,10 @@ __device__ __forceinline__ void load_fwd(StepData& d, const double* M, const dou
   d.w = G[kk * 4 + i];
 }
 
-// ---------------------------------------------------------------------------------------------
-// Blocked solve chains (round 4; the kernels with the blocked factorisation).  Each recurrence of a
-// solve is a chain of H dependent ~100-cycle steps on one quad of wave 0.  Over the factorisation's
-// 8 blocks [k_b, k_{b+1}), one per wave:
-//   backward  p_k = F_k p_{k+1} + w_k:  (A) every block from zero at its end (q_k; the last block is
-//             exact), (B) wave 0: p at every block end from the back, p_{k_b} = q_{k_b} + Phi_b
-//             p_{k_{b+1}}, (C) p_k = q_k + d_k, d_k = F_k d_{k+1} from d = p at the block's end;
-//   forward   x_{k+1} = F_k' x_k + g_k:  (A) every block from zero at its start (r_k; block 0 is
-//             exact), (B) x at every block start, x_{k_{b+1}} = r_{k_{b+1}} + Phi_b' x_{k_b},
-//             (C) x_k = r_k + d_k, d_{k+1} = F_k' d_k from d = x at the block's start;
-// with Phi_b = F_{k_b} ... F_{k_{b+1}-1} (b = 1..6) formed once per factorisation
-// (solve_blocks_prepare).  Chains of <= 8 + 6 + 8 steps instead of H; results differ from the
-// sequential chains by rounding only.  LDS: s.xs (the output rollout's buffer, free from the end of
-// the setup to the rollout): Phi [6][16] @0, block-end values [8][4] @96, block-start values @160.
-constexpr int kSolveBlkMax = 8;  // steps per block (H <= 64)
-static_assert((DRCVAR_MPC_MAX_HORIZON + kBlkW - 1) / kBlkW <= kSolveBlkMax, "solve block length");
-
-__device__ inline void solve_blocks_prepare(const Lds& s, int H) {
-  const int lane = opaque_lane(), w = opaque_wave();
-  if (w < 1 || w > 6) return;
-  double* Phi = s.xs + (w - 1) * 16;
-  const int e = lane & 15, r = e >> 2, c = e & 3;
-  if (lane < 16) Phi[e] = r == c ? 1.0 : 0.0;
-  for (int k = blk_begin(w + 1, H) - 1; k >= blk_begin(w, H); --k) {  // Phi <- F_k Phi
-    wave_lds_fence();
-    double acc = 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc += s.SM[(k * 4 + r) * 4 + m] * Phi[m * 4 + c];
-    wave_lds_fence();
-    if (lane < 16) Phi[e] = acc;
-  }
-}
-
-// One step's operands for the blocked chains: slot q of a block (q < kSolveBlkMax), loaded four
-// steps ahead through a ring of four (all eight at once spilled).  back: step k = ke - 1 - q, row i
-// of F_k; forward: step k = kb + q, column i of F_k; w = src[k][i].  Slots past the block are
-// marked out and read the block's first step (discarded where used).
-__device__ __forceinline__ void blk_load(StepData& d, const double* M, const double* src, int q, int kb,
-                                         int ke, int i, bool back) {
-  const int k = back ? ke - 1 - q : kb + q;
-  d.in = k >= kb && k < ke;
-  const int kk = d.in ? k : kb;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) d.f[m] = back ? M[(kk * 4 + i) * 4 + m] : M[(kk * 4 + m) * 4 + i];
-  d.w = src[kk * 4 + i];
-}
-
-// the backward chain over W (sources in, p_k out); pass (B) sits between two barriers, the
-// caller's barrier ends pass (C)
-__device__ inline void chain_back_blocked(const Lds& s, int H, double* W) {
-  const int lane = opaque_lane(), b = opaque_wave(), i = lane & 3;
-  const double* M = s.SM;
-  double* PE = s.xs + 96;
-  const bool keeper = lane < 4;
-  double* junk = s.T + lane;  // the non-keeper lanes' stores (no branch on the chain)
-  const int kb = blk_begin(b, H), ke = blk_begin(b + 1, H);
-  StepData d[4];
-  {  // (A)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) blk_load(d[q], M, W, q, kb, ke, i, true);
-    double p = 0.0;
-#pragma unroll
-    for (int q = 0; q < kSolveBlkMax; ++q) {
-      StepData& e = d[q & 3];
-      const double pn = affine4(e.w, e.f, p);
-      p = e.in ? pn : p;
-      *(keeper && e.in ? W + (ke - 1 - q) * 4 + i : junk) = p;
-      if (q + 4 < kSolveBlkMax) blk_load(e, M, W, q + 4, kb, ke, i, true);
-    }
-  }
-  __syncthreads();
-  if (b == 0) {  // (B)
-    double p = W[blk_begin(kBlkW - 1, H) * 4 + i];
-    for (int bb = kBlkW - 2; bb >= 1; --bb) {
-      if (keeper) PE[bb * 4 + i] = p;
-      double f[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) f[m] = s.xs[(bb - 1) * 16 + i * 4 + m];
-      p = affine4(W[blk_begin(bb, H) * 4 + i], f, p);
-    }
-    if (keeper) PE[i] = p;
-  }
-  __syncthreads();
-  if (b <= kBlkW - 2) {  // (C)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) blk_load(d[q], M, W, q, kb, ke, i, true);
-    double dl = PE[b * 4 + i];
-#pragma unroll
-    for (int q = 0; q < kSolveBlkMax; ++q) {
-      StepData& e = d[q & 3];
-      const double dn = affine4(0.0, e.f, dl);
-      dl = e.in ? dn : dl;
-      *(keeper && e.in ? W + (ke - 1 - q) * 4 + i : junk) = e.w + dl;
-      if (q + 4 < kSolveBlkMax) blk_load(e, M, W, q + 4, kb, ke, i, true);
-    }
-  }
-}
-
-// the forward chain (sources G, x_k into W[k], x_H into W[H]); as chain_back_blocked
-__device__ inline void chain_fwd_blocked(const Lds& s, int H, double* W, const double* G) {
-  const int lane = opaque_lane(), b = opaque_wave(), i = lane & 3;
-  const double* M = s.SM;
-  double* RE = s.xs + 96;
-  double* XS = s.xs + 160;
-  const bool keeper = lane < 4;
-  double* junk = s.T + lane;
-  const int kb = blk_begin(b, H), ke = blk_begin(b + 1, H);
-  StepData d[4];
-  {  // (A)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) blk_load(d[q], M, G, q, kb, ke, i, false);
-    double r = 0.0;
-#pragma unroll
-    for (int q = 0; q < kSolveBlkMax; ++q) {
-      StepData& e = d[q & 3];
-      *(keeper && e.in ? W + (kb + q) * 4 + i : junk) = r;
-      const double rn = affine4(e.w, e.f, r);
-      r = e.in ? rn : r;
-      if (q + 4 < kSolveBlkMax) blk_load(e, M, G, q + 4, kb, ke, i, false);
-    }
-    if (keeper) RE[b * 4 + i] = r;
-    if (keeper && b == kBlkW - 1) W[H * 4 + i] = r;
-  }
-  __syncthreads();
-  if (b == 0) {  // (B)
-    double x = RE[i];
-    for (int bb = 1; bb <= kBlkW - 2; ++bb) {
-      if (keeper) XS[bb * 4 + i] = x;
-      double f[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) f[m] = s.xs[(bb - 1) * 16 + m * 4 + i];  // row i of Phi_b'
-      x = affine4(RE[bb * 4 + i], f, x);
-    }
-    if (keeper) XS[(kBlkW - 1) * 4 + i] = x;
-  }
-  __syncthreads();
-  if (b >= 1) {  // (C)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) blk_load(d[q], M, W, q, kb, ke, i, false);
-    double dl = XS[b * 4 + i];
-#pragma unroll
-    for (int q = 0; q < kSolveBlkMax; ++q) {
-      StepData& e = d[q & 3];
-      *(keeper && e.in ? W + (kb + q) * 4 + i : junk) = e.w + dl;
-      const double dn = affine4(0.0, e.f, dl);
-      dl = e.in ? dn : dl;
-      if (q + 4 < kSolveBlkMax) blk_load(e, M, W, q + 4, kb, ke, i, false);
-    }
-    if (keeper && b == kBlkW - 1) W[H * 4 + i] += dl;
-  }
-}
-
 // With pos: also the positions the solution produces, pos[2k+i] = c[2k+i] + (C x_{k+1})_i (c may
 // be null: 0) — read off the forward pass's states instead of a separate Mp convolution.
 template <int NU, int kBlock>
-__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c,
-                                         bool blk_form) {
-  const bool blk = kBlockedSolve && kBlock == 512 && blk_form;  // the blocked chains (opt-in build)
+__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c) {
   const int t = threadIdx.x;
   double* W = s.SV;   // [H + 1][4]: Kg_k' b_k, then p_k (backward pass), then x_k (forward pass)
   double* G = s.red;  // [H][4]: B kff_k
@@ -1653,10 +1044,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
     W[e] = acc;
   }
   __syncthreads();
-  if constexpr (kBlockedSolve && kBlock == 512) {
-    if (blk) chain_back_blocked(s, H, W);
-  }
-  if (!blk && t < 64) {  // backward: p_k = F_k p_{k+1} + w_k, row i of F_k
+  if (t < 64) {  // backward: p_k = F_k p_{k+1} + w_k, row i of F_k
     const int i = t & 3;
     // lanes 0..3 store the state; the others write the same instruction into scratch (s.T, one
     // slot per lane), so the chain carries no branch (an exec-masked store split the loop)
@@ -1708,10 +1096,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
     }
   }
   __syncthreads();
-  if constexpr (kBlockedSolve && kBlock == 512) {
-    if (blk) chain_fwd_blocked(s, H, W, G);
-  }
-  if (!blk && t < 64) {  // forward: x_{k+1} = F_k' x_k + B kff_k, column i of F_k
+  if (t < 64) {  // forward: x_{k+1} = F_k' x_k + B kff_k, column i of F_k
     const int i = t & 3;
     const bool keeper = t < 4;
     double xs = 0.0;
@@ -1754,9 +1139,9 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
 // positions of the solution as well, pos = c + Gp x (c may be null).  Ends with a barrier.
 template <int NU, int NX, int kBlock, int HMX>
 __device__ inline void newton_solve(const Lds& s, int H, double* x, double* pos = nullptr,
-                                    const double* c = nullptr, bool blk = false) {
+                                    const double* c = nullptr) {
   if constexpr (NX <= 4) {
-    riccati_solve_dpp<NU, kBlock>(s, H, x, pos, c, blk);
+    riccati_solve_dpp<NU, kBlock>(s, H, x, pos, c);
   } else {
     riccati_solve<NU, NX>(s, H, x);
     if (pos) {
@@ -2032,10 +1417,7 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   // last wave gathers the scalars and checks the digests (lane = record).  (16-B loads of step
   // pairs, two halves of the records per wave, measured slower: the extra live registers spilled.)
   const double* base = cl.xbuf + half;
-#ifndef DRCVAR_CLUSTER_GATHER
-#define DRCVAR_CLUSTER_GATHER 8
-#endif
-  constexpr int kG = DRCVAR_CLUSTER_GATHER;  // agent-scope loads in flight per wave
+  constexpr int kG = 8;  // agent-scope loads in flight per wave (16: no faster)
   for (int q = wave; q < Q; q += kWaves) {
     double v[kG];
     double t = op_identity(step_op);
@@ -2122,9 +1504,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   const int o_lo = CL ? static_cast<int>((static_cast<int64_t>(O) * cid) / cl_size) : 0;
   const int o_hi = CL ? static_cast<int>((static_cast<int64_t>(O) * (cid + 1)) / cl_size) : O;
   const Lds s = carve<kWaves, NU, NX, HMX>(lds_raw);
-  const bool blocked = ric_blocked_form<NX, kWaves>(H);  // blocked Riccati factorisation (uniform)
   const double* H0 = a.blob + a.off.H0;
-  const double* H0T = a.blob + a.off.H0T;  // H0 transposed (the blocked form's rows, rhs_parts)
   double* ws = a.ws + a.ws_off + b * a.ws_pp;
   Cluster cl{};
   if constexpr (CL) {
@@ -2233,24 +1613,6 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     s.u[j] = u0;
   }
   __syncthreads();
-  if constexpr (kBlockedDyn && NX == 4 && kWaves == 8) {
-    // the blocked form's rows take H0 u through the dynamics: AB[i] = A^i B ([H][4][NU] in s.xs,
-    // free from here to the output rollout), by the last wave (first read behind later barriers)
-    if (blocked && wave == kWaves - 1) {
-      const int r = lane / NU, c = lane - (lane / NU) * NU;
-      const bool mine = lane < 4 * NU;
-      double v = mine ? s.Bm[r * NU + c] : 0.0;
-      if (mine) s.xs[lane] = v;
-      for (int i = 1; i < H; ++i) {
-        wave_lds_fence();
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc += s.Am[r * kMx + m] * s.xs[(i - 1) * 4 * NU + m * NU + c];
-        wave_lds_fence();
-        if (mine) s.xs[i * 4 * NU + lane] = acc;
-      }
-    }
-  }
   positions<NU, kBlock>(s, s.u, s.p, s.c, H);
   __syncthreads();
 
@@ -2463,90 +1825,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         rdm = fmax(rdm, fabs(r));
         s.dua[j] = -r - s.rU[j] - gpt_row<NU, kBlock>(s, s.za, nullptr, nullptr, j, n, H);
       };
-      if (blocked) {
-        // The blocked factorisation (round 4): wave 0 forms rows 0..63 of r_du / dua while waves
-        // 1..7 run phase 1, the last wave rows 64.. while wave 0 runs phase 2 (n <= 128)
-        if constexpr (kBlockedCode && NX == 4 && kWaves == 8) {
-#ifdef DRCVAR_MPC_STAMPS
-          unsigned long long bt = __builtin_amdgcn_s_memtime();
-#define BLK_ACC(k)                                                    \
-  do {                                                                \
-    if (blockIdx.x == 0 && lane == 0) {                               \
-      const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
-      g_blk_stamps[wave * 8 + (k)] += now_ - bt;                      \
-      bt = now_;                                                      \
-    }                                                                 \
-  } while (0)
-#else
-#define BLK_ACC(k) \
-  do {             \
-  } while (0)
-#endif
-          // rows of r_du / dua as PARTS partial sums per row (rhs_parts: gpt_row's order), on the
-          // waves phase 3 leaves free: the last from the start of phase 2, the one before it after
-          // its own block; combined after one barrier
-          double* psA = s.red + kBlkW * kBlkSlot;
-          double* psB = psA + kBlkRowParts;
-          const bool dyn = kBlockedDyn && 4 * NU * H <= (DRCVAR_MPC_MAX_HORIZON + 1) * DRCVAR_MPC_MAX_STATES;
-          if constexpr (kBlockedDyn) {
-            if (dyn) {  // H0 u = 2 (Gx' Q Gx u + R u): the states Gx u, then Z = Q Gx u (all threads)
-              double* Xp = psB + kBlkRowParts;  // [H][4][4 parts]
-              double* Zs = Xp + 16 * DRCVAR_MPC_MAX_HORIZON;  // [H][4]
-              for (int e = tid; e < 16 * H; e += kBlock) {
-                const int part = e & 3, k = e >> 4, i = (e >> 2) & 3;
-                double acc = 0.0;
-                for (int j = part; j <= k; j += 4) {
-#pragma unroll
-                  for (int c = 0; c < NU; ++c) acc += s.xs[(k - j) * 4 * NU + i * NU + c] * s.u[j * NU + c];
-                }
-                Xp[e] = acc;
-              }
-              __syncthreads();
-              for (int e = tid; e < 4 * H; e += kBlock) {
-                const int k = e >> 2, i = e & 3;
-                double z = 0.0;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                  const double* xp = Xp + (k * 4 + m) * 4;
-                  z += s.Qm[i * kMx + m] * (((xp[0] + xp[1]) + xp[2]) + xp[3]);
-                }
-                Zs[e] = z;
-              }
-              __syncthreads();
-            }
-          }
-          ric_blocked_phase1<NU>(s, H);
-          if constexpr (kBlockedDyn) {
-            if (dyn && wave == 0)
-              rhs_parts_dyn<NU, kBlock>(s, n, H, psA, psB, psB + kBlkRowParts + 16 * DRCVAR_MPC_MAX_HORIZON, lane, 64);
-          }
-          BLK_ACC(0);
-          __syncthreads();
-          BLK_ACC(1);
-          ric_blocked_phase2(s, H);
-          if (!dyn && wave == kWaves - 1) rhs_parts<NU, kBlock>(s, H0T, n, H, psA, psB, lane, 128);
-          BLK_ACC(2);
-          ric_blocked_phase3<NU>(s, H);
-          if (!dyn && wave == kWaves - 2) rhs_parts<NU, kBlock>(s, H0T, n, H, psA, psB, 64 + lane, 128);
-          BLK_ACC(4);
-          __syncthreads();
-          for (int j = tid; j < n; j += kBlock) {
-            double r = s.f[j] + parts_total<kBlock>(psA, j);
-            if (dyn) {  // + 2 R u (the dynamics form's H0 u carries 2 Gx'Q Gx u in psA)
-              const int jj = j / NU, ai = j - jj * NU;
-              double ru = 0.0;
-#pragma unroll
-              for (int c = 0; c < NU; ++c) ru += s.Rm[ai * NU + c] * s.u[jj * NU + c];
-              r += 2.0 * ru;
-            }
-            if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
-            s.rdu[j] = r;
-            rdm = fmax(rdm, fabs(r));
-            s.dua[j] = -r - s.rU[j] - parts_total<kBlock>(psB, j);
-          }
-#undef BLK_ACC
-        }
-      } else if (wave == 0) {
+      if (wave == 0) {
         riccati_factor_wave0<NU, NX>(s, H);
       } else {
         for (int j = tid - 64; j < n; j += kBlock - 64) rdu_row(j);
@@ -2581,19 +1860,14 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     MPC_PHASE(2);
     // A failed pivot close to the optimum hands over to the polish (the usual end of a solve
     // whose barrier weights have outgrown fp64); further out the stationary form takes over.
-    // (a failed blocked factorisation is repeated sequentially first)
-    if (!(blocked ? ric_blocked_finish<NU, NX>(s, H) : riccati_factor_finish<NU, NX>(s, H)) &&
-        !(blocked && riccati_factor<NU, NX>(s, H)) &&
+    if (!riccati_factor_finish<NU, NX>(s, H) &&
         (best_merit <= kPolishMerit || !riccati_factor<NU, NX, true>(s, H))) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
     CL_NOTE(s.Ri[0]);  // the factorisation (its first pivot's inverse)
     MPC_PHASE(3);
-    if constexpr (kBlockedSolve && NX == 4 && kWaves == 8) {
-      if (blocked) solve_blocks_prepare(s, H);  // (read behind the solve's first barrier)
-    }
-    newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa, nullptr, blocked);  // direction, positions
+    newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa, nullptr);  // direction, positions
     MPC_PHASE(4);
 
     // ---- P2+P3: affine step length, affine gap, corrector rhs — one sweep of the rows ----
@@ -2717,7 +1991,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     const double sigma_mu = s.sc[63];
     MPC_PHASE(5);
-    newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.dp, nullptr, blocked);
+    newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.dp, nullptr);
     MPC_PHASE(4);
 
     // ---- P4: corrector step length ----
@@ -2932,10 +2206,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         __syncthreads();
       }
       MPC_PHASE(10);
-      if (!riccati_factor_any<NU, NX, kWaves>(s, H) && !riccati_factor<NU, NX, true>(s, H)) break;
-      if constexpr (kBlockedSolve && NX == 4 && kWaves == 8) {
-        if (blocked) solve_blocks_prepare(s, H);
-      }
+      if (!riccati_factor<NU, NX>(s, H) && !riccati_factor<NU, NX, true>(s, H)) break;
       CL_NOTE(s.Ri[0]);
       MPC_PHASE(11);
       // The rhs of a pass depends on the multipliers only (the bb terms are at the free response
@@ -2997,7 +2268,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
         __syncthreads();
         MPC_PHASE(12);
-        newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.p, s.c, blocked);  // u and its positions
+        newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.p, s.c);  // u and its positions
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
         MPC_PHASE(13);
@@ -3448,24 +2719,24 @@ int device_cus() {
 #endif
 }  // namespace drcvar_mpc_detail
 
-#if DRCVAR_MPC_HOST_PART
+#if defined(DRCVAR_MPC_STAMPS) && DRCVAR_MPC_DEVICE_PART(2)
+// diagnostic build only (not part of the ABI header): the stamps of the 2-input kernels (the
+// double integrator of every benchmark), exported by the part that holds them
 extern "C" {
-
-#if defined(DRCVAR_MPC_STAMPS) && !defined(DRCVAR_MPC_PART)
-// diagnostic build only (not part of the ABI header)
 int drcvar_diag_cluster_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cl_stamps), sizeof(g_cl_stamps), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 8 : -1;
-}
-int drcvar_diag_blk_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blk_stamps), sizeof(g_blk_stamps), 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 64 : -1;
 }
 int drcvar_diag_mpc_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mpc_stamps), sizeof(g_mpc_stamps), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? kStampProblems : -1;
 }
+}
 #endif
+
+#if DRCVAR_MPC_HOST_PART
+extern "C" {
+
 
 int drcvar_mpc_model_init(const double* A, const double* B, const double* C, const double* Q,
                           const double* R, int32_t nx, int32_t nu, int32_t ny, int32_t H,
@@ -3552,11 +2823,6 @@ int drcvar_mpc_model_init(const double* A, const double* B, const double* C, con
   for (int t = 0; t < H; ++t)
     for (int i = 0; i < nu; ++i)
       for (int j = 0; j < nu; ++j) H0[(t * nu + i) * n + t * nu + j] += 2.0 * R[i * nu + j];
-  {
-    double* H0T = blob + L.H0T;
-    for (int r = 0; r < n; ++r)
-      for (int c = 0; c < n; ++c) H0T[static_cast<int64_t>(c) * n + r] = H0[static_cast<int64_t>(r) * n + c];
-  }
   // F1 = 2 Gx' Qbar Phi  (n x nx),  F2 = 2 Gx' Qbar (n x H*nx)
   double* F1 = blob + L.F1;
   double* F2 = blob + L.F2;

@@ -43,17 +43,6 @@ def npz_problem(path, key):
     return model, h, g, x0, xr, torch.zeros((h.shape[0], H, 2), dtype=torch.float64, device=dev)
 
 
-def blk_stamps():
-    """Cumulative per-wave phase cycles of the blocked factorisation (workgroup 0), or None."""
-    try:
-        f = lib.drcvar_diag_blk_stamps
-    except AttributeError:
-        return None
-    f.argtypes = [ctypes.c_void_p]
-    b = (ctypes.c_ulonglong * 64)()
-    return np.frombuffer(b, dtype=np.uint64).astype(np.int64).reshape(8, 8) if f(ctypes.cast(b, ctypes.c_void_p)) == 64 else None
-
-
 for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
     if shape.startswith("npz:"):  # npz:<path>:<key>
         _, path, key = shape.split(":")
@@ -63,7 +52,6 @@ for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
         H, O, B = (int(v) for v in shape.split(","))
         model, rec, x0, xr, uf = problem_batch(H, O, B, dev)
         h, g = rec[..., 3:5], rec[..., 7]
-    blk0 = blk_stamps()
     x, u, info = mf.filter_batch(model, h, g, x0, xr, uf)
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * (64 * 20))()
@@ -82,10 +70,3 @@ for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
         names = ["partials+barrier", "combine+stores+drain", "barrier", "arrive+poll", "barrier", "gather"]
         print("  cluster exchange sub-phases (cumulative, workgroup 0):",
               ", ".join(f"{n} {cs[i] / max(cs[:6].sum(), 1) * 100:.0f}%" for i, n in enumerate(names)))
-    blk1 = blk_stamps()
-    if blk0 is not None and blk1 is not None and (blk1 - blk0).any():
-        d = (blk1 - blk0) / max(int(st[9]), 1)
-        print("  blocked factorisation per interior-point iteration, workgroup 0 (cycles): wave: "
-              "phase 1 (+rows) / barrier / phase 2 (+rows) / barrier / phase 3")
-        for w in range(8):
-            print(f"    wave {w}: " + " / ".join(f"{v:7.0f}" for v in d[w, :5]))

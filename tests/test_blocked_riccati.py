@@ -1,11 +1,13 @@
-"""CPU check of the algebra behind the MPC kernel's blocked factorisation and blocked solve chains
-(csrc/drcvar_mpc.hip, `ric_blocked_*`, `chain_back_blocked`, `chain_fwd_blocked`):
-a NumPy restatement of exactly those steps — the same 8 block bounds (w H) // 8, the zero-terminal
-element recursion (J_E, A_E, C_E), the block-end map P_s = J_E + A_E' (I + P_e C_E)^-1 P_e A_E by
-elimination without pivoting, each block's recursion rerun from its true end value, and the
-three-pass chains through the block products Phi_b — against the sequential Riccati recursion and a
-dense solve of the condensed system K du = b, on LQ problems shaped like the interior-point method's
-Newton systems (double integrator, per-step output weights S_k, input weights growing to 1e8).
+"""CPU check of the algebra behind the blocked Riccati factorisation and blocked solve chains that
+round 4 measured in the MPC kernel and did not keep (the kernel code is in git
+history, commit 2f6f9c7): a NumPy restatement of exactly those steps — the same 8 block bounds
+(w H) // 8, the zero-terminal element recursion (J_E, A_E, C_E), the block-end map
+P_s = J_E + A_E' (I + P_e C_E)^-1 P_e A_E by elimination without pivoting, each block's recursion
+rerun from its true end value, and the three-pass chains through the block products Phi_b — against
+the sequential Riccati recursion and a dense solve of the condensed system K du = b, on LQ problems
+shaped like the interior-point method's Newton systems (double integrator, per-step output weights
+S_k, input weights growing to 1e8).  Also H0 u through the dynamics (two convolutions) against the
+blob's condensed H0.
 
 The reference's QP (core/mpc_filter.py:114-151) is solved by OSQP through CVXPY; the kernel
 replaces it, and this test pins only the restructured linear algebra, not the interior-point method.
@@ -215,7 +217,7 @@ def test_blocked_factorisation_and_solve_match_sequential(H, scale, seed):
 
 
 def test_h0u_through_the_dynamics_matches_the_blob():
-    """The DRCVAR_BLOCKED_DYN rows form H0 u as 2 (Gx' Q (Gx u) + R u) from an A^i B table — two
+    """H0 u as 2 (Gx' Q (Gx u) + R u) from an A^i B table (round 4's dynamics variant) — two
     convolutions instead of the condensed n x n H0 that drcvar_mpc_model_init stores in the blob.
     Same numbers (to rounding) as the blob's H0 times u, for the reference's double integrator."""
     from tests.test_mpc import model_init

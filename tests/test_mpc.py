@@ -176,11 +176,7 @@ def test_model_init_condensation(dyn):
         o += want.size
     assert blob[o] == 1.0
     o += 1
-    # H0 transposed, bit for bit (the blocked form's affine-rhs rows read its columns)
-    n = nu * H
-    h0 = blob[:n * n].reshape(n, n)
-    np.testing.assert_array_equal(blob[o:o + n * n].reshape(n, n), h0.T)
-    assert o + n * n == m.blob_doubles
+    assert o == m.blob_doubles
 
 
 def test_model_init_bounds_and_validation():
