@@ -1741,6 +1741,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // round should follow.  Inlined at both call sites (a loop around it, or an out-of-line
   // function, made the compiler spill inside the interior-point loop: C5 QP +5 % / +40 %).
   auto ipm_round = [&](const int round) __attribute__((always_inline)) -> bool {
+  bool converged = false;  // this round's loop met its tolerance (the factorisation beside it stands)
   // positions of the starting (or restored) iterate and its P1 row pass
   positions<NU, kBlock>(s, s.u, s.p, s.c, H);
   __syncthreads();
@@ -1841,6 +1842,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       const double merit = fmax(fmax(rp / scale_d, rd / scale_q), mu);
       CL_NOTE(merit);
       if (merit <= tol_r) {
+        converged = true;
         status = DRCVAR_MPC_STATUS_OPTIMAL;
         best_merit = merit;
         break;
@@ -2118,18 +2120,45 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // conditions fail are moved (primal-dual active-set step), up to kPolishAttempts times.  On
   // success the answer is exact to roundoff; otherwise the interior-point answer stands.
   const bool tried = a.polish && best_merit <= kPolishMerit && !(CL && cl.aborted);
+  // The active-set guess from the predictor (round 5).  On the iteration that met the tolerance
+  // wave 0 has factorised the Newton matrix beside the affine rhs (s.dua), so one solve gives the
+  // affine direction at the endpoint, and every complementary pair (w, lambda) is classified by
+  // Tapia's indicators: active when d lambda / lambda > d w / w (its w heading to zero faster than
+  // its lambda).  The endpoint's own lambda > w misreads rows whose slack is small but positive
+  // (lambda_s ~ 0.1 against s ~ 5e-4 at merit 2e-8 on the bench's C5 instance): the first polish
+  // attempt then fails and a second one is paid.  Counted on the CPU restatement
+  // (scripts/micro/classify_lab.py, 110 problems: C5 DR-CVaR, main.py's three metrics at C5 and
+  // H = 20 sizes, 64 batch seeds, few-obstacle problems) against the KKT-certified optimum: lambda > w
+  // misclassifies 11 pairs in 8 problems, the indicators none.  Without a usable factorisation (a
+  // stalled or resumed-from-best endpoint, a failed pivot) the endpoint rule stands.
+  bool predicted = false;
+  if (tried && converged) {
+    if (riccati_factor_finish<NU, NX>(s, H)) {  // uniform
+      newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa, nullptr);  // affine du (in place), dp
+      predicted = true;
+    }
+    CL_NOTE(predicted ? 1.0 : 0.0);
+  }
   if (tried) {
     for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];  // the answer if polishing fails
     // classify: flag 0 = halfspace not binding (s = 0), 1 = slack positive (s = h.p + g > 0),
     // 2 = binding with s = 0 (equality, multiplier nu in [0, 50]); rows.s <- nu, rows.wA <- flag
     if (lane < K) {
+      const double p0 = s.p[2 * lane], p1 = s.p[2 * lane + 1];
+      const double a0 = predicted ? s.dpa[2 * lane] : 0.0, a1 = predicted ? s.dpa[2 * lane + 1] : 0.0;
       for (int o = o_lo + wave; o < o_hi; o += kWaves) {
         const int64_t r = static_cast<int64_t>(o) * kRowStride + lane;
-        const bool actA = rows.lA[r] > rows.wA[r], actB = rows.lB[r] > rows.wB[r];
+        const HsRow q = rows.load(r);
+        bool actA = q.lA > q.wA, actB = q.lB > q.wB;
+        if (predicted) {  // Tapia's indicators on the affine direction
+          const RowDir d = hs_affine(q, hs_lin(q, p0, p1), q.h0 * a0 + q.h1 * a1);
+          actA = d.dlA * q.wA > d.dwA * q.lA;
+          actB = d.dlB * q.wB > d.dwB * q.lB;
+        }
         const double flag = actA ? (actB ? 2.0 : 1.0) : 0.0;
-        SAVED_S[r] = rows.s[r];
-        SAVED_W[r] = rows.wA[r];
-        rows.s[r] = flag == 2.0 ? rows.lA[r] : 0.0;
+        SAVED_S[r] = q.sv;
+        SAVED_W[r] = q.wA;
+        rows.s[r] = flag == 2.0 ? q.lA : 0.0;
         rows.wA[r] = flag;
       }
     }
@@ -2137,7 +2166,13 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     if (a.has_u) {
       for (int j = tid; j < n; j += kBlock) {
         const PairState q = box_state(s, n, j);
-        const bool up = q.lu > q.wu, lo = q.ll > q.wl;
+        bool up = q.lu > q.wu, lo = q.ll > q.wl;
+        if (predicted) {
+          const int ai = j % NU;
+          const PairDir d = pair_dir(q, pair_lin(q, s.u[j], a.umin[ai], a.umax[ai]), 0.0, s.dua[j], 0.0, false);
+          up = d.dlu * q.wu > d.dwu * q.lu;
+          lo = d.dll * q.wl > d.dwl * q.ll;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) SAVED_B[k * n + j] = s.bx[k * n + j];
         s.bx[j] = up;
@@ -2149,7 +2184,13 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     if (a.has_p) {
       for (int t = tid; t < 2 * H; t += kBlock) {
         const PairState q = pos_state(s, H, t);
-        const bool up = q.lu > q.wu, lo = q.ll > q.wl;
+        bool up = q.lu > q.wu, lo = q.ll > q.wl;
+        if (predicted) {
+          const int i = t & 1;
+          const PairDir d = pair_dir(q, pair_lin(q, s.p[t], a.pmin[i], a.pmax[i]), 0.0, s.dpa[t], 0.0, false);
+          up = d.dlu * q.wu > d.dwu * q.lu;
+          lo = d.dll * q.wl > d.dwl * q.ll;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) SAVED_B[4 * n + k * 2 * H + t] = s.px[k * 2 * H + t];
         s.px[t] = up;
