@@ -135,6 +135,23 @@ def _compile_units():
     return units
 
 
+def source_key(basename: str = "drcvar_halfspace.hip") -> str:
+    """A hash of one translation unit's inputs (its source, every header and .inc table it can
+    include, its extra compile flags): profiles/ evidence is tied to the kernel code it measured,
+    and bench.py uses it only while the sources still match."""
+    import glob
+    import hashlib
+    src = os.path.join(PKG_DIR, "csrc", basename)
+    incs = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.inc")))
+    h = hashlib.sha256(open(src, "rb").read())
+    for f in HEADERS + incs:
+        h.update(open(f, "rb").read())
+    for s, defs in _compile_units():
+        if s == src:
+            h.update(" ".join(defs).encode())
+    return h.hexdigest()[:16]
+
+
 def build(verbose: bool = False, extra_flags=()) -> str:
     """Compile the engine for gfx950 with hipcc into ``_lib/`` (works without a GPU).
 

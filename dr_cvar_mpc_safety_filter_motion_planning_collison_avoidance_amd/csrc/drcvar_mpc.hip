@@ -147,7 +147,10 @@ constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:
 constexpr double kStepFrac = 0.995;
 constexpr double kHuge = 1e300;
 constexpr int kPerStepQ = 7;          // per-step partial sums carried by one reduction
-constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
+#ifndef DRCVAR_POLISH_RHO  // diagnostic A/B builds may move it
+#define DRCVAR_POLISH_RHO 1e6
+#endif
+constexpr double kPolishRho = DRCVAR_POLISH_RHO;    // method-of-multipliers penalty of the polish
 constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
@@ -189,6 +192,17 @@ enum { kSiteStart = 1, kSiteP1, kSiteP23, kSiteP4, kSitePolishHess, kSitePolishR
 constexpr int kStampProblems = 64, kStampSlots = 20;
 __device__ unsigned long long g_mpc_stamps[kStampProblems * kStampSlots];
 __device__ unsigned long long g_cl_stamps[8];  // cluster exchange sub-phases, problem 0, group 0
+// per-wave spans of the P1 phase (workgroup 0 of problem 0): [wave][0] = cycles from the barrier
+// before the factorisation to the wave's end of its P1 work, summed over iterations; [wave][1] = count
+__device__ unsigned long long g_wave_stamps[16];
+#define WAVE_SPAN_BEGIN() const unsigned long long wspan0_ = __builtin_amdgcn_s_memtime()
+#define WAVE_SPAN_END()                                                                     \
+  do {                                                                                      \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 8) {              \
+      atomicAdd(&g_wave_stamps[2 * (threadIdx.x >> 6)], __builtin_amdgcn_s_memtime() - wspan0_); \
+      atomicAdd(&g_wave_stamps[2 * (threadIdx.x >> 6) + 1], 1ull);                          \
+    }                                                                                       \
+  } while (0)
 #define CL_STAMP(k)                                                     \
   do {                                                                  \
     if (threadIdx.x == 0 && blockIdx.x == 0) {                          \
@@ -211,6 +225,12 @@ __device__ unsigned long long g_cl_stamps[8];  // cluster exchange sub-phases, p
   } while (0)
 #define MPC_PHASE(k) \
   do {               \
+  } while (0)
+#define WAVE_SPAN_BEGIN() \
+  do {                    \
+  } while (0)
+#define WAVE_SPAN_END() \
+  do {                  \
   } while (0)
 #endif
 
@@ -672,7 +692,29 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[N
 // Wave 0's part: the recursion (Kg, Ri into LDS; s.sc[62] = 0 on success, 1 on a failed pivot).
 // No barrier: the interior-point loop runs it beside the other waves' work (riccati_factor below
 // is the plain form: this, a barrier, riccati_factor_finish).
-template <int NU, int NX, bool kStationary = false>
+#ifdef DRCVAR_NO_PIPE  // diagnostic A/B builds: the affine solve after the factorisation
+constexpr bool kPipe = false;
+#else
+constexpr bool kPipe = true;
+#endif
+// The progress words of the pipelined affine solve (int slots in s.sc[56..57]): the factorisation's
+// last finished step and the dual-residual wave's last finished input step (both count down from
+// H; kProgAbort after a failed pivot, which releases the follower).
+constexpr int kProgAbort = -1000;
+__device__ __forceinline__ int* prog_word(const Lds& s, int q) { return reinterpret_cast<int*>(s.sc + 56 + q); }
+__device__ __forceinline__ void prog_publish(const Lds& s, int q, int k) {
+  wave_lds_fence();  // the step's stores (LDS, one wave: completed in issue order) before the word
+  __hip_atomic_store(prog_word(s, q), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // every lane
+}
+// (a poll is one LDS read; between polls the waiting wave sleeps ~256 cycles, a quarter of a
+// factorisation step, so that its reads do not queue in front of the factorisation's own)
+__device__ __forceinline__ void prog_wait(const Lds& s, int q, int k) {
+  while (__hip_atomic_load(prog_word(s, q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > k)
+    __builtin_amdgcn_s_sleep(4);
+  wave_lds_fence();
+}
+
+template <int NU, int NX, bool kStationary = false, bool kPublish = false>
 __device__ inline void riccati_factor_wave0(const Lds& s, int H) {
   const int tid = threadIdx.x, lane = tid & 63;
   double* flag = s.sc + 62;
@@ -817,8 +859,12 @@ __device__ inline void riccati_factor_wave0(const Lds& s, int H) {
 #pragma unroll
           for (int d = 0; d < NU; ++d) s.Ri[(k * NU + c) * NU + d] = Ri[c][d];
       }
+      if constexpr (kPublish) prog_publish(s, 0, k);  // Kg_k, Ri_k are out
     }
     if (lane == 0) *flag = ok ? 0.0 : 1.0;
+    if constexpr (kPublish) {
+      if (!ok) prog_publish(s, 0, kProgAbort);
+    }
   }
 }
 
@@ -1030,17 +1076,28 @@ __device__ __forceinline__ void load_fwd(StepData& d, const double* M, const dou
 
 // With pos: also the positions the solution produces, pos[2k+i] = c[2k+i] + (C x_{k+1})_i (c may
 // be null: 0) — read off the forward pass's states instead of a separate Mp convolution.
+// With z (per-step 2-vectors, [2H]): K x = b - Gp' z without forming Gp' z — z_k is the linear
+// cost C'z_k on the state x_{k+1} of the LQ problem, so it enters the backward pass as a source,
+// p_k = C'z_{k-1} + F_k p_{k+1} + Kg_k' b_k with p_H = C'z_{H-1} (the value function's linear term),
+// instead of a Gp' z convolution (n rows of ~H / PARTS terms) and its two barriers.
+// Two halves: dpp_backward leaves kff_k = -Re_k^-1 (B' p_{k+1} - b_k) in x and the forward
+// sources B kff_k in s.red; dpp_forward runs the forward recurrence and writes du = kff - Kg x.
+// (The interior-point loop's affine solve runs the backward half beside the factorisation,
+// affine_backward_follow, and only the forward half after it.)
 template <int NU, int kBlock>
-__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c) {
+__device__ inline void dpp_backward(const Lds& s, int H, double* x, const double* z) {
   const int t = threadIdx.x;
-  double* W = s.SV;   // [H + 1][4]: Kg_k' b_k, then p_k (backward pass), then x_k (forward pass)
+  double* W = s.SV;   // [H + 1][4]: Kg_k' b_k (+ C'z_{k-1}), then p_k (backward pass)
   double* G = s.red;  // [H][4]: B kff_k
   const double* M = s.SM;
-  for (int e = t; e < H * 4; e += kBlock) {
+  for (int e = t; e < (H + 1) * 4; e += kBlock) {
     const int k = e >> 2, i = e & 3;
     double acc = 0.0;
+    if (k < H) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) acc += s.Kg[(k * NU + u) * 4 + i] * x[k * NU + u];
+      for (int u = 0; u < NU; ++u) acc += s.Kg[(k * NU + u) * 4 + i] * x[k * NU + u];
+    }
+    if (z && k >= 1) acc += s.Cm[i] * z[2 * k - 2] + s.Cm[kMx + i] * z[2 * k - 1];
     W[e] = acc;
   }
   __syncthreads();
@@ -1049,7 +1106,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
     // lanes 0..3 store the state; the others write the same instruction into scratch (s.T, one
     // slot per lane), so the chain carries no branch (an exec-masked store split the loop)
     const bool keeper = t < 4;
-    double p = 0.0;
+    double p = W[H * 4 + i];  // p_H: C'z_{H-1} (0 without z)
     const int Hp = (H + 3) & ~3;  // W holds HM >= Hp steps
     StepData d[4];
 #pragma unroll
@@ -1058,7 +1115,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // step k - q; its data was loaded four steps ago
         const double pn = affine4(d[q].w, d[q].f, p);
-        p = d[q].in ? pn : p;      // the padding steps (k >= H) keep p_H = 0
+        p = d[q].in ? pn : p;      // the padding steps (k >= H) keep p_H
         *(keeper ? W + (k - q) * 4 + i : s.T + t) = p;  // p_k (w_k was read four steps ago)
         load_back(d[q], M, W, k - q - 4, i, H);
       }
@@ -1072,10 +1129,8 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
 #pragma unroll
     for (int c = 0; c < NU; ++c) {
       double acc = -x[k * NU + c];
-      if (k + 1 < H) {
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc += s.Bm[m * NU + c] * W[(k + 1) * 4 + m];
-      }
+      for (int m = 0; m < 4; ++m) acc += s.Bm[m * NU + c] * W[(k + 1) * 4 + m];  // p_H = W[H]
       ge[c] = acc;
     }
     double gi = 0.0;
@@ -1096,6 +1151,17 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
     }
   }
   __syncthreads();
+}
+
+// The forward half: x_{k+1} = F_k' x_k + B kff_k from x_0 = 0 (F_k in s.SM, B kff_k in s.red),
+// du_k = kff_k - Kg_k x_k into du (kff may be du), the positions into pos.  Ends with a barrier.
+template <int NU, int kBlock>
+__device__ inline void dpp_forward(const Lds& s, int H, const double* kff, double* du, double* pos,
+                                   const double* c) {
+  const int t = threadIdx.x;
+  double* W = s.SV;   // [H + 1][4]: x_k
+  const double* G = s.red;
+  const double* M = s.SM;
   if (t < 64) {  // forward: x_{k+1} = F_k' x_k + B kff_k, column i of F_k
     const int i = t & 3;
     const bool keeper = t < 4;
@@ -1118,10 +1184,10 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
   // du_k = kff_k - Kg_k x_k
   for (int e = t; e < H * NU; e += kBlock) {
     const int k = e / NU, u = e - (e / NU) * NU;
-    double acc = x[e];
+    double acc = kff[e];
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc -= s.Kg[(k * NU + u) * 4 + m] * W[k * 4 + m];
-    x[e] = acc;
+    du[e] = acc;
   }
   if (pos) {  // p_k = c_k + C x_{k+1}
     for (int e = t; e < 2 * H; e += kBlock) {
@@ -1135,19 +1201,204 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
   __syncthreads();
 }
 
-// K x = b: the DPP recurrences for NX <= 4, the wave-serial recursion otherwise.  With pos: the
-// positions of the solution as well, pos = c + Gp x (c may be null).  Ends with a barrier.
+template <int NU, int kBlock>
+__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c,
+                                         const double* z) {
+  dpp_backward<NU, kBlock>(s, H, x, z);
+  dpp_forward<NU, kBlock>(s, H, x, x, pos, c);
+}
+
+// K x = b - Gp' z (z may be null): the DPP recurrences for NX <= 4 (z as a state source), the
+// wave-serial recursion otherwise (Gp' z summed first).  With pos: the positions of the solution as
+// well, pos = c + Gp x (c may be null).  Ends with a barrier.
 template <int NU, int NX, int kBlock, int HMX>
-__device__ inline void newton_solve(const Lds& s, int H, double* x, double* pos = nullptr,
-                                    const double* c = nullptr) {
+__device__ inline void newton_solve(const Lds& s, int H, int n, double* x, double* pos = nullptr,
+                                    const double* c = nullptr, const double* z = nullptr) {
   if constexpr (NX <= 4) {
-    riccati_solve_dpp<NU, kBlock>(s, H, x, pos, c);
+    riccati_solve_dpp<NU, kBlock>(s, H, x, pos, c, z);
   } else {
+    if (z) {
+      gpt_parts<NU, kBlock>(s, z, nullptr, nullptr, s.red, n, H);
+      __syncthreads();
+      for (int j = threadIdx.x; j < n; j += kBlock) x[j] -= parts_total<kBlock>(s.red, j);
+      __syncthreads();
+    }
     riccati_solve<NU, NX>(s, H, x);
     if (pos) {
       positions<NU, kBlock>(s, x, pos, c, H);
       __syncthreads();
     }
+  }
+}
+
+// The dual residual of the inputs r_du = f + H0 u + Gp' v + (lUu - lUl) and the input part of the
+// affine rhs, dua = -r_du - rU (its Gp' za part goes to the solve as a state source), for NX <= 4 on
+// ONE wave, without the condensed H0: H0 u = 2 R u + 2 Gx' Q Gx u and Gp' v = Gx' C' v, so with the
+// states of u from x_0 = 0 (forward: x_{k+1} = A x_k + B u_k) and the adjoint (backward:
+// lambda_H = y_H, lambda_k = y_k + A' lambda_{k+1}, y_k = 2 Q x_k + C' v_{k-1}),
+//   r_du_j = f_j + 2 (R u)_j + B' lambda_{j+1} (+ box).
+// Phases of one wave (wave-local LDS hand-offs, no barrier): the sources B u_k for every step at
+// once; the forward chain (lane i of each quad holds x_i, quad broadcasts, the source loaded four
+// steps ahead as in the solves); y_k for every step at once; the backward chain; r_du for every
+// input at once — two chains of H ~100-cycle steps instead of n rows of ~H + n dependent LDS terms
+// (~33 k cycles at C5 on seven waves).  Progress word 1 is set once at the end.  X: 8 (H + 1)
+// doubles of scratch.  Returns this lane's max |r_du|.
+template <int NU>
+__device__ inline double dual_residual_wave(const Lds& s, int H, int n, bool has_u, double* X) {
+  const int lane = threadIdx.x & 63, i = lane & 3;
+  const bool keeper = lane < 4;
+  double* Src = X;                // [H + 1][4]: B u_k (at k), then y_k
+  double* Xs = X + (H + 1) * 4;   // [H + 1][4]: x_k, then lambda_k
+  // the other lanes' copy of each chain store (no exec-mask branch in the chain): s.dp, free from
+  // the previous update to this iteration's corrector solve (s.T is the concurrent factorisation's)
+  double* junk = s.dp + lane;
+  for (int e = lane; e < H * 4; e += 64) {  // Src[k] = B u_k
+    const int k = e >> 2, r = e & 3;
+    double w = 0.0;
+#pragma unroll
+    for (int c = 0; c < NU; ++c) w += s.Bm[r * NU + c] * s.u[k * NU + c];
+    Src[e] = w;
+  }
+  wave_lds_fence();
+  double arow[4], acol[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    arow[m] = s.Am[i * kMx + m];
+    acol[m] = s.Am[m * kMx + i];
+  }
+  const int Hp = (H + 3) & ~3;
+  {  // forward: x_{k+1} = A x_k + B u_k, x_0 = 0
+    double x = 0.0, w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = Src[(q < H ? q : 0) * 4 + i];
+    for (int k = 0; k < Hp; k += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double xn = affine4(w[q], arow, x);
+        x = k + q < H ? xn : x;
+        *(keeper ? Xs + (k + q + 1) * 4 + i : junk) = x;  // x_{k+q+1}
+        const int kn = k + q + 4;
+        w[q] = Src[(kn < H ? kn : 0) * 4 + i];
+      }
+    }
+  }
+  wave_lds_fence();
+  for (int e = lane + 4; e < (H + 1) * 4; e += 64) {  // y_k = 2 Q x_k + C' v_{k-1}, k >= 1 (in place)
+    const int k = e >> 2, r = e & 3;
+    double y = s.Cm[r] * s.v[2 * k - 2] + s.Cm[kMx + r] * s.v[2 * k - 1];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) y += 2.0 * s.Qm[r * kMx + m] * Xs[k * 4 + m];
+    Src[e] = y;  // (Src's B u_k are no longer needed; y_k lands in Src, lambda_k in Xs)
+  }
+  wave_lds_fence();
+  {  // backward: lambda_k = y_k + A' lambda_{k+1}, lambda_{H+1} = 0
+    double lam = 0.0, y[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = H - q;
+      y[q] = Src[(kk >= 1 ? kk : 1) * 4 + i];
+    }
+    for (int k = H; k >= H + 1 - Hp; k -= 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = k - q;
+        const double ln = affine4(y[q], acol, lam);
+        lam = kk >= 1 ? ln : lam;
+        *(keeper && kk >= 1 ? Xs + kk * 4 + i : junk) = lam;  // lambda_kk
+        const int kn = kk - 4;
+        y[q] = Src[(kn >= 1 ? kn : 1) * 4 + i];
+      }
+    }
+  }
+  wave_lds_fence();
+  double rdm = 0.0;
+  for (int j = lane; j < n; j += 64) {
+    const int jj = j / NU, ai = j - jj * NU;
+    double ru = 0.0;
+#pragma unroll
+    for (int c = 0; c < NU; ++c) ru += s.Rm[ai * NU + c] * s.u[jj * NU + c];
+    double r = s.f[j] + 2.0 * ru;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) r += s.Bm[m * NU + ai] * Xs[(jj + 1) * 4 + m];
+    if (has_u) r += s.bx[n + j] - s.bx[3 * n + j];
+    s.rdu[j] = r;
+    rdm = fmax(rdm, fabs(r));
+    s.dua[j] = -r - s.rU[j];
+  }
+  prog_publish(s, 1, -1);  // every input step's rows are out
+  return rdm;
+}
+
+// The backward half of the affine solve (dpp_backward with b = dua, z = za), run by one wave beside
+// the factorisation and one step behind it: step k waits for the factorisation's Kg_k / Ri_k
+// (progress word 0) and the dual-residual wave's b_k (word 1), then forms row i of the solve map
+// F_k = A' - Kg_k' B' (into s.SM for the later solves), p_k = F_k p_{k+1} + Kg_k' b_k + C'z_{k-1},
+// kff_k = -Re_k^-1 (B' p_{k+1} - b_k) (into kff) and the forward source B kff_k (into s.red).
+// ~40 instructions per step against the factorisation's ~900-cycle step, so after the
+// factorisation only the forward half is left (~7 k cycles of the affine solve's ~17 k).
+template <int NU>
+__device__ inline void affine_backward_follow(const Lds& s, int H, const double* b, const double* z,
+                                              double* kff) {
+  const int lane = threadIdx.x & 63, i = lane & 3;
+  const bool keeper = lane < 4;
+  double acol[4], Bm[4][NU], brow[NU];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    acol[c] = s.Am[c * kMx + i];  // A[c][i]: row i of A'
+#pragma unroll
+    for (int u = 0; u < NU; ++u) Bm[c][u] = s.Bm[c * NU + u];
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) brow[u] = s.Bm[i * NU + u];
+  const double c0 = s.Cm[i], c1 = s.Cm[kMx + i];
+  double p = z ? c0 * z[2 * H - 2] + c1 * z[2 * H - 1] : 0.0;  // p_H = C'z_{H-1}
+  prog_wait(s, 1, -1);  // every b_k (the dual-residual wave publishes once, early)
+  for (int k = H - 1; k >= 0; --k) {
+    prog_wait(s, 0, k);
+    double kgi[NU], bk[NU], ri[NU][NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      kgi[u] = s.Kg[(k * NU + u) * 4 + i];
+      bk[u] = b[k * NU + u];
+#pragma unroll
+      for (int v = 0; v < NU; ++v) ri[u][v] = s.Ri[(k * NU + u) * NU + v];
+    }
+    const int kz = k >= 1 ? 2 * k - 2 : 0;  // C'z_{k-1} (k >= 1), loaded with the rest
+    const double zc = z ? c0 * z[kz] + c1 * z[kz + 1] : 0.0;
+    double fr[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double acc = acol[c];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) acc -= kgi[u] * Bm[c][u];
+      fr[c] = acc;
+    }
+    if (keeper) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s.SM[(k * 4 + i) * 4 + c] = fr[c];
+    }
+    double w = 0.0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) w += kgi[u] * bk[u];
+    w += k >= 1 ? zc : 0.0;
+    const double pv0 = quad_bcast_f64<0x00>(p), pv1 = quad_bcast_f64<0x55>(p);
+    const double pv2 = quad_bcast_f64<0xAA>(p), pv3 = quad_bcast_f64<0xFF>(p);  // p_{k+1}
+    double ge[NU], gi = 0.0, mine = 0.0;
+#pragma unroll
+    for (int v = 0; v < NU; ++v) ge[v] = Bm[0][v] * pv0 + Bm[1][v] * pv1 + Bm[2][v] * pv2 + Bm[3][v] * pv3 - bk[v];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      double acc = 0.0;
+#pragma unroll
+      for (int v = 0; v < NU; ++v) acc -= ri[u][v] * ge[v];
+      gi += brow[u] * acc;
+      mine = i == u ? acc : mine;
+    }
+    if (keeper) {
+      s.red[k * 4 + i] = gi;
+      if (i < NU) kff[k * NU + i] = mine;
+    }
+    p = fma(fr[0], pv0, fma(fr[1], pv1, w)) + fma(fr[2], pv2, fr[3] * pv3);
   }
 }
 
@@ -1581,6 +1832,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     s.f[j] = acc;
   }
+  MPC_PHASE(17);  // setup: model, c, x_ref staging, f
   // starting inputs: the tracking optimum without rows, u = -H0^-1 f = UF1 x0 + UF2 xr (condensed
   // on the host), strictly inside the input box; the UF2 x_ref sums as interleaved partial sums
   // (threads (j, part)), so no thread carries a chain of H nx loads
@@ -1628,6 +1880,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // bench-like DR-CVaR C5 problems 78 -> 64 iterations over six seeds (the degenerate C5 fixture
   // 14 -> 10), main.py's three filters at C5 size and H = 20 / 10 obstacles 180 -> 151 (C5 mean
   // 50 -> 50, C5 CVaR 42 -> 33), main.py-like problems with 3-10 obstacles 106 -> 76.
+  MPC_PHASE(18);  // setup: starting inputs and their positions
   const bool many_rows = O >= kManyRowsObstacles;
   const double mu0 = many_rows ? kStartMuMany : kStartMuFew;
   double gmax = 0.0;
@@ -1674,13 +1927,23 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       gmax = fmax(gmax, fmax(fabs(a.pmin[i]), fabs(a.pmax[i])));
     }
   }
+  MPC_PHASE(19);  // setup: the rows' and bounds' starting points
   double fmaxv = 0.0;
   for (int j = tid; j < n; j += kBlock) fmaxv = fmax(fmaxv, fabs(s.f[j]));
   if constexpr (CL) {  // |g| over every row of the problem: each workgroup reads all of hs_g (a
-    // cluster exchange before round 4; a maximum is exact in any order, so every workgroup agrees)
+    // cluster exchange before round 4; a maximum is exact in any order, so every workgroup agrees),
+    // eight loads in flight per lane (one at a time, a C5 workgroup waited for 32 in series)
     if (lane < K) {
-      for (int o = wave; o < O; o += kWaves)
-        gmax = fmax(gmax, fabs(a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk]));
+      for (int o0 = wave; o0 < O; o0 += 8 * kWaves) {
+        double gv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int o = o0 + q * kWaves;
+          gv[q] = o < O ? a.hs_g[b * a.g_sp + o * a.g_so + lane * a.g_sk] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) gmax = fmax(gmax, fabs(gv[q]));
+      }
     }
   }
   {
@@ -1813,24 +2076,42 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
           s.rU[j] = 0.0;
         }
       }
+      if (tid == 0) {  // the pipelined affine solve's progress words (no step finished yet)
+        *prog_word(s, 0) = H;
+        *prog_word(s, 1) = H;
+      }
       __syncthreads();
       // Wave 0 factorises K (it needs S and DU only) while the other waves form the dual residual
-      // of the inputs r_du = H0 u + f + Gp' v + (lUu - lUl) and the affine rhs dua, one thread per
-      // input (gpt_row: the partial-sum order of gpt_parts).  The factorisation is speculative:
-      // on the iteration whose merit meets the tolerance it is not used (round 4: it used to wait
-      // for those two Gp' products and their three barriers).
-      auto rdu_row = [&](int j) {
-        double r = s.f[j] + gpt_row<NU, kBlock>(s, s.v, H0, s.u, j, n, H);
-        if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
-        s.rdu[j] = r;
-        rdm = fmax(rdm, fabs(r));
-        s.dua[j] = -r - s.rU[j] - gpt_row<NU, kBlock>(s, s.za, nullptr, nullptr, j, n, H);
-      };
+      // of the inputs r_du = H0 u + f + Gp' v + (lUu - lUl) and the input part of the affine rhs,
+      // dua = -r_du - rU (its Gp' za part enters the solve as a state source).  For NX <= 4 wave 1
+      // alone, by the two recurrences of dual_residual_wave (round 5); otherwise one thread per
+      // input (gpt_row: the partial-sum order of gpt_parts).  The factorisation is speculative: on
+      // the iteration whose merit meets the tolerance it serves the polish's active-set guess.
+      // For NX <= 4 a third wave (wave 1 after its rows in the 128-thread form) runs the backward
+      // half of the affine solve one step behind the factorisation (affine_backward_follow: kff
+      // into s.du, the forward sources into s.red, the solve maps into s.SM), so that after it only
+      // the forward half is left (round 5).  The waves hand over through the progress words.
+      WAVE_SPAN_BEGIN();
       if (wave == 0) {
-        riccati_factor_wave0<NU, NX>(s, H);
+        riccati_factor_wave0<NU, NX, false, NX <= 4 && kPipe>(s, H);
+      } else if constexpr (NX <= 4) {
+        if (wave == 1) rdm = fmax(rdm, dual_residual_wave<NU>(s, H, n, a.has_u, s.xs));
+        if (kPipe && wave == (kWaves >= 3 ? 2 : 1)) affine_backward_follow<NU>(s, H, s.dua, s.za, s.du);
       } else {
-        for (int j = tid - 64; j < n; j += kBlock - 64) rdu_row(j);
+        // (NX > 4 keeps the affine rhs's Gp' za in these rows: handing it to the solve as for
+        // the other systems made the 4-input, 8-state kernels diverge on every problem of
+        // test_gpu_many_problems_every_form[generic4] — those kernels spill ~350-550 VGPRs, and
+        // the same sums in newton_solve, by gpt_parts or gpt_row, with or without an extra
+        // barrier, all failed, while this form passes; round 5)
+        for (int j = tid - 64; j < n; j += kBlock - 64) {
+          double r = s.f[j] + gpt_row<NU, kBlock>(s, s.v, H0, s.u, j, n, H);
+          if (a.has_u) r += s.bx[n + j] - s.bx[3 * n + j];
+          s.rdu[j] = r;
+          rdm = fmax(rdm, fabs(r));
+          s.dua[j] = -r - s.rU[j] - gpt_row<NU, kBlock>(s, s.za, nullptr, nullptr, j, n, H);
+        }
       }
+      WAVE_SPAN_END();
       block_sum_max_max<kWaves>(gap, rpm, rdm, s.sc);  // its barriers also end the factorisation
       mu = m_ineq > 0.0 ? gap / m_ineq : 0.0;
       rp = rpm;
@@ -1862,14 +2143,22 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     MPC_PHASE(2);
     // A failed pivot close to the optimum hands over to the polish (the usual end of a solve
     // whose barrier weights have outgrown fp64); further out the stationary form takes over.
-    if (!riccati_factor_finish<NU, NX>(s, H) &&
+    // (NX <= 4: when the factorisation succeeded, the pipelined backward half of the affine solve
+    // has run beside it and left the solve maps; only the forward half follows)
+    const bool piped = kPipe && NX <= 4 && s.sc[62] == 0.0;  // uniform
+    if (!piped && !riccati_factor_finish<NU, NX>(s, H) &&
         (best_merit <= kPolishMerit || !riccati_factor<NU, NX, true>(s, H))) {
       status = DRCVAR_MPC_STATUS_NUMERICAL;
       break;
     }
     CL_NOTE(s.Ri[0]);  // the factorisation (its first pivot's inverse)
     MPC_PHASE(3);
-    newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa, nullptr);  // direction, positions
+    if constexpr (NX <= 4) {
+      if (piped) dpp_forward<NU, kBlock>(s, H, s.du, s.dua, s.dpa, nullptr);  // direction, positions
+      else newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.dua, s.dpa, nullptr, s.za);
+    } else {  // (dua holds the whole rhs, Gp' za included)
+      newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.dua, s.dpa);
+    }
     MPC_PHASE(4);
 
     // ---- P2+P3: affine step length, affine gap, corrector rhs — one sweep of the rows ----
@@ -1982,18 +2271,15 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       CL_NOTE(a_aff);
       CL_NOTE(sigma_mu);
       s.sc[63] = sigma_mu;  // same value in every thread; kept for P4/P5
-      // Gp' is linear: Gp' za + sigma_mu Gp' zu = Gp' (za + sigma_mu zu), combined in place
+      // Gp' is linear: Gp' za + sigma_mu Gp' zu = Gp' (za + sigma_mu zu), combined in place and
+      // handed to the solve as its state source
       for (int t = tid; t < 2 * H; t += kBlock) s.zu[t] = s.za[t] + sigma_mu * s.zu[t];
-      __syncthreads();
-      gpt_parts<NU, kBlock>(s, s.zu, nullptr, nullptr, s.red, n, H);
-      __syncthreads();
-      for (int j = tid; j < n; j += kBlock)
-        s.du[j] = -s.rdu[j] - (s.rU[j] + sigma_mu * s.rUu[j]) - parts_total<kBlock>(s.red, j);
+      for (int j = tid; j < n; j += kBlock) s.du[j] = -s.rdu[j] - (s.rU[j] + sigma_mu * s.rUu[j]);
       __syncthreads();
     }
     const double sigma_mu = s.sc[63];
     MPC_PHASE(5);
-    newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.dp, nullptr);
+    newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.du, s.dp, nullptr, s.zu);
     MPC_PHASE(4);
 
     // ---- P4: corrector step length ----
@@ -2133,8 +2419,16 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // stalled or resumed-from-best endpoint, a failed pivot) the endpoint rule stands.
   bool predicted = false;
   if (tried && converged) {
-    if (riccati_factor_finish<NU, NX>(s, H)) {  // uniform
-      newton_solve<NU, NX, kBlock, HMX>(s, H, s.dua, s.dpa, nullptr);  // affine du (in place), dp
+    bool done = false;
+    if constexpr (NX <= 4 && kPipe) {
+      if (s.sc[62] == 0.0) {  // uniform: the backward half ran beside the factorisation
+        dpp_forward<NU, kBlock>(s, H, s.du, s.dua, s.dpa, nullptr);  // affine du, dp
+        predicted = done = true;
+      }
+    }
+    if (!done && riccati_factor_finish<NU, NX>(s, H)) {  // uniform
+      // affine du (in place), dp; NX > 4: dua holds the whole rhs
+      newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.dua, s.dpa, nullptr, NX <= 4 ? s.za : nullptr);
       predicted = true;
     }
     CL_NOTE(predicted ? 1.0 : 0.0);
@@ -2295,11 +2589,10 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
             s.za[t] = z;
           }
         }
-        __syncthreads();
-        gpt_parts<NU, kBlock>(s, s.za, nullptr, nullptr, s.red, n, H);
-        __syncthreads();
+        // the input part of the rhs (-f and the bound terms; the per-step za is the solve's state
+        // source)
         for (int j = tid; j < n; j += kBlock) {
-          double r = -s.f[j] - parts_total<kBlock>(s.red, j);
+          double r = -s.f[j];
           if (a.has_u) {
             const int ai = j % NU;
             if (s.bx[j] != 0.0) r -= s.bx[n + j] - kPolishRho * a.umax[ai];
@@ -2309,7 +2602,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         }
         __syncthreads();
         MPC_PHASE(12);
-        newton_solve<NU, NX, kBlock, HMX>(s, H, s.du, s.p, s.c);  // u and its positions
+        newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.du, s.p, s.c, s.za);  // u and its positions
         for (int j = tid; j < n; j += kBlock) s.u[j] = s.du[j];
         __syncthreads();
         MPC_PHASE(13);
@@ -2771,6 +3064,10 @@ int drcvar_diag_cluster_stamps(unsigned long long* host) {
 int drcvar_diag_mpc_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mpc_stamps), sizeof(g_mpc_stamps), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? kStampProblems : -1;
+}
+int drcvar_diag_wave_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_stamps), sizeof(g_wave_stamps), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 16 : -1;
 }
 }
 #endif

@@ -19,7 +19,7 @@ if [ "$src" = drcvar_mpc ]; then
       $tmp/csrc/$src.hip -o $tmp/part_$k.o &
     new+=($tmp/part_$k.o)
   done
-  wait
+  for j in $(jobs -p); do wait $j || { echo "a part failed to compile" >&2; exit 1; }; done
 else
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -I $tmp/include $tmp/csrc/$src.hip -o $tmp/one.o
   new+=($tmp/one.o)

@@ -15,7 +15,7 @@ if [ "$src" = drcvar_mpc ]; then
       $PKG/csrc/$src.hip -o /tmp/variant_${name}_$k.o &
     new+=(/tmp/variant_${name}_$k.o)
   done
-  wait
+  for j in $(jobs -p); do wait $j || { echo "a part failed to compile" >&2; exit 1; }; done
 else
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -I include "$@" $PKG/csrc/$src.hip -o /tmp/variant_$name.o
   new+=(/tmp/variant_$name.o)

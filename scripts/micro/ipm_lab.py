@@ -178,7 +178,10 @@ def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False, 
         gap_aff = sum(((state[k][0] + a_aff * d_a[k][0]) * (state[k][1] + a_aff * d_a[k][1])).sum()
                       for k in state)
         sigma_mu = (gap_aff / gap) ** START.get("sig_exp", 3.0) * mu
-        rc = {k: -w_ * l_ - d_a[k][0] * d_a[k][1] + sigma_mu for k, (w_, l_) in state.items()}
+        if variant.startswith("nosoc"):  # no second-order correction: corrector = affine + sigma mu unit
+            rc = {k: -w_ * l_ + sigma_mu for k, (w_, l_) in state.items()}
+        else:
+            rc = {k: -w_ * l_ - d_a[k][0] * d_a[k][1] + sigma_mu for k, (w_, l_) in state.items()}
         du, ds, d = direction(rc)
         amax = amax_of(d)
         if variant == "gondzio":

@@ -20,7 +20,8 @@ NAMES = {0: "setup", 1: "P1 residuals+weights", 2: "affine rhs", 3: "Riccati fac
          4: "Riccati solves (ipm)", 5: "row passes P2-P5", 6: "loop exit", 7: "polish other",
          8: "output", 10: "polish classify+assemble", 11: "polish Riccati factor",
          12: "polish row passes", 13: "polish solves", 14: "positions (ipm)", 15: "loop top",
-         16: "cluster exchanges"}
+         16: "cluster exchanges", 17: "setup: model, c, x_ref, f", 18: "setup: u start + positions",
+         19: "setup: rows' start"}
 dev = torch.device("cuda", 0)
 lib = _native.lib()
 lib.drcvar_diag_mpc_stamps.argtypes = [ctypes.c_void_p]
@@ -70,3 +71,13 @@ for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
         names = ["partials+barrier", "combine+stores+drain", "barrier", "arrive+poll", "barrier", "gather"]
         print("  cluster exchange sub-phases (cumulative, workgroup 0):",
               ", ".join(f"{n} {cs[i] / max(cs[:6].sum(), 1) * 100:.0f}%" for i, n in enumerate(names)))
+    try:
+        ws = lib.drcvar_diag_wave_stamps
+        ws.argtypes = [ctypes.c_void_p]
+        wb = (ctypes.c_ulonglong * 16)()
+        if ws(ctypes.cast(wb, ctypes.c_void_p)) == 16:
+            w = np.frombuffer(wb, dtype=np.uint64).astype(np.int64).reshape(8, 2)
+            print("  P1 span per wave (cumulative over launches so far, cycles per entry): " +
+                  ", ".join(f"w{i} {w[i, 0] / max(w[i, 1], 1):.0f}" for i in range(8) if w[i, 1]))
+    except AttributeError:
+        pass

@@ -258,6 +258,10 @@ def _random_problem(rng, O, T, H, dyn="double", bounds=True, tight=True):
         A = np.eye(4) + 0.01 * rng.normal(size=(4, 4))
         B = 0.2 * rng.normal(size=(4, 3))
         C = np.eye(4)[:2]
+    elif dyn == "generic44":  # four inputs on the 4-state template (the widest NX <= 4 kernels)
+        A = np.eye(4) + 0.01 * rng.normal(size=(4, 4))
+        B = 0.2 * rng.normal(size=(4, 4))
+        C = np.eye(4)[:2]
     elif dyn == "generic8":  # the widest state (padded template NX = 8), a dense output map
         A = np.eye(8) + 0.01 * rng.normal(size=(8, 8))
         B = 0.2 * rng.normal(size=(8, 2))
@@ -376,7 +380,8 @@ def test_gpu_three_metrics_one_launch(path, dev):
     ("double", 7, 5, 12, True, True), ("double", 20, 4, 9, False, True),
     ("double", 25, 0, 0, True, True), ("single", 60, 8, 60, True, True),
     ("generic1", 64, 4, 64, True, True), ("generic3", 40, 5, 40, True, True),
-    ("generic4", 30, 5, 30, True, True), ("generic8", 24, 4, 24, False, True),
+    ("generic4", 30, 5, 30, True, True), ("generic44", 30, 5, 30, True, True),
+    ("generic8", 24, 4, 24, False, True),
 ])
 def test_gpu_random_problems_match_oracle(dyn, H, O, T, bounds, tight, dev):
     rng = np.random.default_rng(H * 1000 + O * 10 + T)
@@ -427,7 +432,7 @@ def test_gpu_batch_and_strided_views_and_determinism(dev):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dyn,H,O", [("double", 30, 3), ("double", 32, 6), ("double", 40, 4),
                                      ("single", 20, 5), ("generic1", 32, 4), ("generic3", 24, 3),
-                                     ("generic4", 30, 4), ("generic8", 16, 3)])
+                                     ("generic4", 30, 4), ("generic44", 30, 4), ("generic8", 16, 3)])
 def test_gpu_many_problems_every_form(dyn, H, O, dev):
     """More than kFewProblems (128) problems per launch: H <= 32 takes the 128-thread form (its own
     LDS plan), longer horizons the 256-thread form; the same problems launched in chunks of <= 128
