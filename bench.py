@@ -592,26 +592,6 @@ def sampler_roofline(sb, stream, reps=10):
            "kernel_ms": sec * 1e3, "samples_per_s": n / sec, "bound": SAMPLER_BOUND,
            "achieved": written / sec / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
            "frac": written / sec / HBM_PEAK}
-    # draw + evaluate in one launch (drcvar_sample_and_evaluate_f64): the samples drawn in
-    # registers, never written; its records must equal the evaluation of the refilled batch
-    sb.compute()
-    rec = torch.empty((sb.count, 8), dtype=torch.float64, device=sb.samples.device)
-    fused = lambda: obstacles.sample_and_evaluate_device(sb.nominal, sb.N, sb.start, sb.count,
-                                                         sb.ego_units, sb.params, seed=sb.seed, out=rec)
-    fused()
-    torch.cuda.synchronize()
-    a.record(stream)
-    for _ in range(reps):
-        fused()
-    b.record(stream)
-    torch.cuda.synchronize()
-    fsec = a.elapsed_time(b) * 1e-3 / reps
-    out["fused_draw_evaluate"] = {
-        "kernel_ms": fsec * 1e3, "halfspaces_per_s": sb.count / fsec,
-        "records_equal_to_refill_then_evaluate": bool(torch.equal(rec, sb.local_records())),
-        "what": "drcvar_sample_and_evaluate_f64: the refill's draws made in registers and evaluated "
-                "in the same launch (no sample written or read); compare with kernel_ms (refill) + "
-                "roofline_large.kernel_ms (evaluate)"}
     return out
 
 

@@ -82,7 +82,6 @@ EXPORTED_SYMBOLS = (
     "drcvar_mpc_filter_f64_ex",
     "drcvar_sample_trajectories_f64",
     "drcvar_sample_units_f64",
-    "drcvar_sample_and_evaluate_f64",
 )
 
 
@@ -249,10 +248,6 @@ def _bind(lib):
     lib.drcvar_sample_units_f64.argtypes = [
         ptr, i64, i64, i64, i64, i64, i64, i64, dbl, dbl, dbl, u64, u64, i32, ptr, i64, i64, ptr]
     lib.drcvar_sample_units_f64.restype = ctypes.c_int
-    lib.drcvar_sample_and_evaluate_f64.argtypes = [
-        ptr, i64, i64, i64, i64, i64, i64, i64, dbl, dbl, dbl, u64, u64, i32, ptr, i64,
-        dbl, dbl, dbl, dbl, dbl, ptr, ptr, ptr]
-    lib.drcvar_sample_and_evaluate_f64.restype = ctypes.c_int
     return lib
 
 

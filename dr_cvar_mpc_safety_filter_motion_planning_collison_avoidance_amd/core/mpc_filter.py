@@ -144,6 +144,10 @@ def filter_batch(model: MPCModel, hs_h: torch.Tensor, hs_g: torch.Tensor, x0: to
     u_fallback [B, H, nu].  Returns (x [B, H+1, nx], u [B, H, nu], info [B, 10]) device tensors
     (columns ``_native.MPC_INFO_*``); nothing is synchronised.  ``polish`` finishes each solve
     with the active-set polish (exact optimum when it succeeds).  ``options``: :func:`make_options`.
+    A clustered problem whose workgroups could not all stay resident, or disagreed, ends
+    CLUSTER_TIMEOUT / CLUSTER_DIVERGED with the fallback rolled out; this function does not retry
+    it — batch callers call :func:`retry_cluster_failures` on the result themselves (the
+    MPCSafetyFilter wrapper does).
     """
     dev = model.device
     B = x0.shape[0]

@@ -29,12 +29,10 @@
 // No MFMA: ~10 flops per 16-B sample — the kernel is bounded by HBM.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cmath>
 #include <cstdint>
 
 #include "drcvar_halfspace.h"
-#include "drcvar_sampling.h"
 
 namespace {
 
@@ -42,12 +40,8 @@ constexpr int kWave = 64;
 constexpr int kCap = 128;          // candidates ranked directly (per-wave region size in LDS)
 constexpr int kMaxValueIters = 3;  // value-linear refinements before switching to integer keys
 constexpr double kSentinel = 100.0;
-#ifndef DRCVAR_PAIR_MAX  // diagnostic builds may move it (0: every slot its own Philox call)
-#define DRCVAR_PAIR_MAX 12288
-#endif
-constexpr int kPairMax = DRCVAR_PAIR_MAX;  // generating plans up to this many slots draw in pairs (LDS staging)
-// sample load forms (kernel template); kLoadGen: no loads, the samples are drawn in registers
-constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2, kLoadGen = 3;
+// sample load forms (kernel template)
+constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2;
 #ifndef DRCVAR_NT_BYTES  // diagnostic builds may move the threshold (scripts/micro A/B runs)
 #define DRCVAR_NT_BYTES (256ll << 20)
 #endif
@@ -56,21 +50,6 @@ constexpr int64_t kNtBytes = DRCVAR_NT_BYTES;  // launches reading more than the
 #define DRCVAR_HS_LDS_PAD 0
 #endif
 typedef double dbl2 __attribute__((ext_vector_type(2)));
-
-#include "drcvar_generator.inc"
-
-// The generating form (kLoadGen, drcvar_sample_and_evaluate_f64): unit k of the launch is unit
-// u0 + k of a global [O, T] batch, whose samples are drawn in registers exactly as
-// drcvar_sample_units_f64 draws them (Philox counter base unit * pairs, pairs = ceil(N/2)) —
-// the samples never exist in memory.
-struct GenArgs {
-  const double* nominal;
-  int64_t nom_so, nom_st, T, u0;
-  uint64_t pairs;
-  double l00, l10, l11;
-  uint32_t k0, k1, s0, s1;
-  int zero_first;
-};
 
 #ifdef DRCVAR_STAMPS
 // diagnostic build only: per-unit shader-clock stamps at phase boundaries (wave 0)
@@ -638,8 +617,7 @@ __device__ __forceinline__ double rank_candidates(const double* cand, uint32_t c
 // instead of keeping register state live: exact min/max, then histogram refinement (value-linear,
 // then order-preserving integer keys) until <= kCap candidates remain or the run collapses to one
 // value.  Result (valid in wave 0): tau and dsum = sum_{d<tau} (d - tau).
-// proj(i): the projection h . xi_i of sample i (re-read from memory, or drawn again by the
-// generating form).
+// proj(i): the projection h . xi_i of sample i (re-read from memory).
 template <int BLOCK, int LOG_NB, class Proj>
 __device__ __forceinline__ void select_from_memory(const Proj& proj, int n, double mu_d,
                                                 uint32_t rank, uint32_t* hist, double* cand,
@@ -809,8 +787,7 @@ __global__ void __launch_bounds__(BLOCK)
 safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
                       int64_t s_obs, int64_t s_step, int64_t s_samp,
                       const double* __restrict__ dir, int64_t dir_s_obs, int64_t dir_s_step,
-                      Params prm, double* __restrict__ out, int32_t* __restrict__ status,
-                      GenArgs gen) {
+                      Params prm, double* __restrict__ out, int32_t* __restrict__ status) {
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << LOG_NB;
   __shared__ uint32_t hist[hist_words<NB>()];
@@ -852,67 +829,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // one 64-bit product for the thread's first sample, then a uniform step per row (the clamp is a
   // select, not a product per sample: the per-sample quarter-rate multiplies sat before the
   // loads were issued).
-  // the generating form: this unit's draw (its nominal point, Philox counter base, the tables)
-  constexpr bool kGen = LOAD == kLoadGen;
-  __shared__ double s_turn[kGen ? kTurnLen : 1], s_log[kGen ? 2 * kLogIdx : 1];
-  double gnx = 0.0, gny = 0.0;
-  uint64_t gg0 = 0;
-  bool gzero = false;
-  if constexpr (kGen) {
-    const int64_t ug = gen.u0 + u;
-    const int64_t og = ug / gen.T, tg = ug - og * gen.T;
-    const double* nom = gen.nominal + og * gen.nom_so + tg * gen.nom_st;
-    gnx = nom[0];
-    gny = nom[1];
-    gzero = gen.zero_first && tg == 0;  // noise-free step 0 (simulation/obstacles.py:63)
-    gg0 = static_cast<uint64_t>(ug) * gen.pairs;
-    load_generator_tables(s_turn, s_log, BLOCK);
-    __syncthreads();
-  }
-  auto draw = [&](int i, double* xv, double* yv) {
-    if (gzero) {
-      *xv = gnx;
-      *yv = gny;
-    } else {
-      generate_sample(gg0, gen.pairs, i, gen.s0, gen.s1, gen.k0, gen.k1, gnx, gny, gen.l00,
-                      gen.l10, gen.l11, s_turn, s_log, xv, yv);
-    }
-  };
   double x[P], y[P];
-  // Paired draws (plans with BLOCK P <= kPairMax): one Philox call gives samples i and i + pairs
-  // (pairs = ceil(N/2)); the thread holding i < pairs draws both, keeps i and hands i + pairs to
-  // its owner through LDS (extern staging [pairs] of 16 B, one barrier) — half the Philox work of
-  // one call per sample, the same values.
-  constexpr bool kPaired = kGen && BLOCK * P <= kPairMax;
-  extern __shared__ dbl2 gen_stage[];
-  if constexpr (kPaired) {
-    if (!gzero) {
-      const int pairs = static_cast<int>(gen.pairs);
-#pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < pairs) {
-          double x2, y2;
-          generate_pair(gg0, i, gen.s0, gen.s1, gen.k0, gen.k1, gnx, gny, gen.l00, gen.l10,
-                        gen.l11, s_turn, s_log, &x[j], &y[j], &x2, &y2);
-          if (i + pairs < n) gen_stage[i] = dbl2{x2, y2};
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < P; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i >= pairs && i < n) {
-          const dbl2 v = gen_stage[i - pairs];
-          x[j] = v.x;
-          y[j] = v.y;
-        } else if (i >= n) {  // idle slot (masked by every sum): the nominal point, no LDS read
-          x[j] = gnx;
-          y[j] = gny;
-        }
-      }
-    }
-  }
   const int64_t off0 = static_cast<int64_t>(tid) * s_samp;
   const int64_t row_step = static_cast<int64_t>(BLOCK) * s_samp;
   const int64_t off_last = static_cast<int64_t>(n - 1) * s_samp;
@@ -920,14 +837,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   for (int j = 0; j < P; ++j) {
     const int i = tid + j * BLOCK;
     const int64_t off = i < n ? off0 + j * row_step : off_last;
-    if constexpr (kPaired) {  // drawn above (gzero: the nominal point)
-      if (gzero) {
-        x[j] = gnx;
-        y[j] = gny;
-      }
-    } else if constexpr (kGen) {  // drawn, not loaded (idle slots draw sample n - 1, as they would load it)
-      draw(i < n ? i : n - 1, &x[j], &y[j]);
-    } else if constexpr (LOAD == kLoadNt) {  // streamed once: keep it out of L2 / MALL
+    if constexpr (LOAD == kLoadNt) {  // streamed once: keep it out of L2 / MALL
       const dbl2 v = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(base + off));
       x[j] = v.x;
       y[j] = v.y;
@@ -950,12 +860,8 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double e0 = dp[0], e1 = dp[1];
   double px = 0.0, py = 0.0;  // row-0 moments' pivot: the unit's first sample
   if constexpr (!kPilot) {
-    if constexpr (kGen) {
-      draw(0, &px, &py);
-    } else {
-      px = base[0];
-      py = base[1];
-    }
+    px = base[0];
+    py = base[1];
   }
   const double inv_n = prm.inv_n, inv_n0 = prm.inv_n0, deg_sq = prm.degenerate_sq;
   const double z_lo = prm.z_lo, hist_scale = prm.hist_scale;
@@ -1189,19 +1095,9 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       }
     }
     if (!settled) {
-      if constexpr (kGen) {  // the exact fallback draws the unit's samples again
-        const auto proj = [&](int i) {
-          double xv, yv;
-          draw(i, &xv, &yv);
-          return project(h0, h1, xv, yv);
-        };
-        select_from_memory<BLOCK, LOG_NB>(proj, n, mu_d, rank, hist, cand, wcount, red_rng, red_tail,
-                                          &tau, &dsum);
-      } else {
-        const auto proj = [&](int i) { return project_at<LOAD != kLoadPair>(base, i, s_samp, h0, h1); };
-        select_from_memory<BLOCK, LOG_NB>(proj, n, mu_d, rank, hist, cand, wcount, red_rng, red_tail,
-                                          &tau, &dsum);
-      }
+      const auto proj = [&](int i) { return project_at<LOAD != kLoadPair>(base, i, s_samp, h0, h1); };
+      select_from_memory<BLOCK, LOG_NB>(proj, n, mu_d, rank, hist, cand, wcount, red_rng, red_tail,
+                                        &tau, &dsum);
     }
     if (wave != 0) {
       if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
@@ -1345,34 +1241,16 @@ struct Launch {
   double* out;
   int32_t* status;  // [units] or null
   hipStream_t stream;
-  GenArgs gen{};          // the generating form's draw (generate = true)
-  bool generate = false;  // samples drawn in registers (kLoadGen), `samples` unused
 };
 
 // grid (n_steps, obstacles), at most kMaxGridY obstacles per launch (the y-dimension limit):
 // larger batches are split into obstacle chunks on the host
 constexpr int64_t kMaxGridY = 65535;
-constexpr int kMaxDevices = 64;  // per-device state of the launcher (the dynamic-LDS attribute)
 
 template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
 int launch_form(const Launch& L) {
   const int64_t n_obs = L.units / L.n_steps;
-  size_t dyn = DRCVAR_HS_LDS_PAD;
-  if constexpr (LOAD == kLoadGen && BLOCK * P <= kPairMax) {
-    // the paired draws' staging: [pairs] of 16 B (80 KB at N = 10 000: above the default 64 KB
-    // limit of dynamic LDS, raised once per kernel and device; a failure is a launch error)
-    dyn = static_cast<size_t>(L.gen.pairs) * 16;
-    static std::atomic<bool> attr_set[kMaxDevices] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return DRCVAR_ERR_LAUNCH;
-    if (!attr_set[dev].load(std::memory_order_acquire)) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(kPairMax / 2 * 16)) != hipSuccess)
-        return DRCVAR_ERR_LAUNCH;
-      attr_set[dev].store(true, std::memory_order_release);
-    }
-  }
+  const size_t dyn = DRCVAR_HS_LDS_PAD;
   for (int64_t o0 = 0; o0 < n_obs; o0 += kMaxGridY) {
     const int64_t chunk = n_obs - o0 < kMaxGridY ? n_obs - o0 : kMaxGridY;
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
@@ -1381,7 +1259,7 @@ int launch_form(const Launch& L) {
                        static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
                        L.dir + o0 * L.dir_s_obs, L.dir_s_obs, L.dir_s_step, L.prm,
                        L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH,
-                       L.status ? L.status + o0 * L.n_steps : nullptr, L.gen);
+                       L.status ? L.status + o0 * L.n_steps : nullptr);
   }
   return DRCVAR_OK;
 }
@@ -1394,9 +1272,6 @@ int launch_plan(Launch L, bool vec) {
   // measured on C5 (2.05 GB): nontemporal 16-B loads 0.746 of HBM peak vs 0.715; on C3 (3.2 MB,
   // cache-resident across steps) they cost 3 %, so only launches larger than the MALL use them
   const bool nt = vec && L.units * L.n * 16 > kNtBytes;
-  if constexpr (!GIVEN_H) {
-    if (L.generate) return launch_form<BLOCK, P, LOG_NB, kLoadGen, false>(L);
-  }
   if (nt) return launch_form<BLOCK, P, LOG_NB, kLoadNt, GIVEN_H>(L);
   if (vec) return launch_form<BLOCK, P, LOG_NB, kLoadVec, GIVEN_H>(L);
   return launch_form<BLOCK, P, LOG_NB, kLoadPair, GIVEN_H>(L);
@@ -1422,7 +1297,7 @@ int dispatch(const Launch& L, int threads, int per) {
   const bool vec = (reinterpret_cast<uintptr_t>(L.samples) % 16 == 0) && (L.s_obs % 2 == 0) &&
                    (L.s_step % 2 == 0) && (L.s_samp % 2 == 0);
   if (L.n > DRCVAR_MAX_SAMPLES) {  // beyond the register plans: the streaming kernel
-    if (threads != 0 || per != 0 || L.generate) return DRCVAR_ERR_UNSUPPORTED;
+    if (threads != 0 || per != 0) return DRCVAR_ERR_UNSUPPORTED;
     if (L.n > DRCVAR_MAX_SAMPLES_STREAM) return DRCVAR_ERR_UNSUPPORTED;
     (void)hipGetLastError();
     launch_stream<GIVEN_H>(L, vec);
@@ -1528,66 +1403,9 @@ int safe_halfspaces(const double* samples, int64_t n_obstacles, int64_t n_steps,
   return dispatch<false>(L, threads, per);
 }
 
-// Units [unit_begin, unit_begin + unit_count) of the global [O, T] batch `nominal` describes,
-// drawn in registers as drcvar_sample_units_f64 draws them and evaluated in the same launch.
-int sample_and_evaluate(const double* nominal, int64_t n_obstacles, int64_t n_steps,
-                        int64_t nom_so, int64_t nom_st, int64_t unit_begin, int64_t unit_count,
-                        int64_t n_samples, double l00, double l10, double l11, uint64_t seed,
-                        uint64_t stream_offset, int32_t zero_first_step, const double* ego_units,
-                        int64_t ego_su, double robot_radius, double obstacle_radius, double alpha,
-                        double delta, double epsilon, double* out, int32_t* status, void* stream) {
-  if (n_obstacles < 0 || n_steps < 0 || n_samples < 1 || unit_begin < 0 || unit_count < 0)
-    return DRCVAR_ERR_INVALID_ARGUMENT;
-  if (!params_ok(robot_radius, obstacle_radius, alpha, delta, epsilon))
-    return DRCVAR_ERR_INVALID_ARGUMENT;
-  if (!(l00 == l00) || !(l10 == l10) || !(l11 == l11)) return DRCVAR_ERR_INVALID_ARGUMENT;
-  if (n_obstacles > (int64_t{1} << 40) || n_steps > (int64_t{1} << 40) ||
-      n_obstacles * n_steps > (int64_t{1} << 40))
-    return DRCVAR_ERR_UNSUPPORTED;
-  if (n_samples > DRCVAR_MAX_SAMPLES) return DRCVAR_ERR_UNSUPPORTED;  // register plans only
-  const int64_t units = n_obstacles * n_steps;
-  if (unit_begin > units || unit_count > units - unit_begin) return DRCVAR_ERR_INVALID_ARGUMENT;
-  if (unit_count == 0) return DRCVAR_OK;
-  if (!nominal || !ego_units || !out || unit_count > 0x7fffffff) return DRCVAR_ERR_INVALID_ARGUMENT;
-  // the launch is one "obstacle" of unit_count steps (grid x = unit), ego per unit
-  Launch L{nullptr, unit_count, unit_count, n_samples, 0, 0, 0, ego_units, 0, ego_su,
-           make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
-           status, static_cast<hipStream_t>(stream)};
-  L.generate = true;
-  L.gen.nominal = nominal;
-  L.gen.nom_so = nom_so;
-  L.gen.nom_st = nom_st;
-  L.gen.T = n_steps;
-  L.gen.u0 = unit_begin;
-  L.gen.pairs = static_cast<uint64_t>((n_samples + 1) >> 1);
-  L.gen.l00 = l00;
-  L.gen.l10 = l10;
-  L.gen.l11 = l11;
-  L.gen.k0 = static_cast<uint32_t>(seed);
-  L.gen.k1 = static_cast<uint32_t>(seed >> 32);
-  L.gen.s0 = static_cast<uint32_t>(stream_offset);
-  L.gen.s1 = static_cast<uint32_t>(stream_offset >> 32);
-  L.gen.zero_first = zero_first_step != 0;
-  return dispatch<false>(L, 0, 0);
-}
-
 }  // namespace
 
 extern "C" {
-
-int drcvar_sample_and_evaluate_f64(const double* nominal, int64_t n_obstacles, int64_t n_steps,
-                                   int64_t nom_so, int64_t nom_st, int64_t unit_begin,
-                                   int64_t unit_count, int64_t n_samples, double l00, double l10,
-                                   double l11, uint64_t seed, uint64_t stream_offset,
-                                   int32_t zero_first_step, const double* ego_units,
-                                   int64_t ego_su, double robot_radius, double obstacle_radius,
-                                   double alpha, double delta, double epsilon, double* out,
-                                   int32_t* status, void* stream) {
-  return sample_and_evaluate(nominal, n_obstacles, n_steps, nom_so, nom_st, unit_begin,
-                             unit_count, n_samples, l00, l10, l11, seed, stream_offset,
-                             zero_first_step, ego_units, ego_su, robot_radius, obstacle_radius,
-                             alpha, delta, epsilon, out, status, stream);
-}
 
 #ifdef DRCVAR_STAMPS
 // diagnostic build only (not part of the ABI header): copy the phase stamps to the host

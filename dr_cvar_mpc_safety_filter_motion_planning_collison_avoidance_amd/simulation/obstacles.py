@@ -155,51 +155,6 @@ def sample_units_device(nominal, n_samples, unit_begin, unit_count, noise_cov=NO
     return out
 
 
-def sample_and_evaluate_device(nominal, n_samples, unit_begin, unit_count, ego_units, params,
-                               noise_cov=NOISE_COV, seed=0, stream_offset=0, zero_first_step=True,
-                               out=None, status=None, stream=None):
-    """Draw + evaluate in one launch (``drcvar_sample_and_evaluate_f64``): the records ``[unit_count,
-    8]`` of units ``[unit_begin, unit_begin + unit_count)`` of the global batch ``nominal`` ``[O, T,
-    2]``, whose samples are drawn in registers exactly as :func:`sample_units_device` draws them —
-    bit for bit the records of ``sample_units_device`` followed by the engine on its output, with
-    no sample ever written to memory.  ``ego_units`` ``[unit_count, 2]``: the ego position per unit;
-    ``params``: :class:`engine.RiskParams`.  ``status`` (optional int32 ``[unit_count]``) receives the
-    per-unit DRCVAR_UNIT_* word."""
-    if not isinstance(nominal, torch.Tensor) or nominal.device.type != "cuda":
-        raise ValueError("nominal must be a device tensor (the sampler has no CPU path)")
-    if nominal.dtype != torch.float64 or nominal.dim() != 3 or nominal.shape[2] != 2 or \
-            nominal.stride(2) != 1:
-        raise ValueError("nominal must be float64 [O, T, 2] with adjacent coordinates")
-    O, T, _ = nominal.shape
-    unit_begin, unit_count, n_samples = int(unit_begin), int(unit_count), int(n_samples)
-    if unit_begin < 0 or unit_count < 0 or unit_begin + unit_count > O * T:
-        raise ValueError(f"unit range [{unit_begin}, {unit_begin + unit_count}) outside the "
-                         f"{O} x {T} batch")
-    if not isinstance(ego_units, torch.Tensor) or ego_units.device != nominal.device or \
-            ego_units.dtype != torch.float64 or tuple(ego_units.shape) != (unit_count, 2) or \
-            ego_units.stride(1) != 1:
-        raise ValueError("ego_units must be a float64 [units, 2] device tensor with adjacent coordinates")
-    L = np.linalg.cholesky(np.asarray(noise_cov, dtype=np.float64).reshape(2, 2))
-    if out is None:
-        out = torch.empty((unit_count, 8), dtype=torch.float64, device=nominal.device)
-    elif tuple(out.shape) != (unit_count, 8) or out.dtype != torch.float64 or \
-            not out.is_contiguous() or out.device != nominal.device:
-        raise ValueError("out must be a contiguous float64 [units, 8] device tensor")
-    if status is not None and (tuple(status.shape) != (unit_count,) or status.dtype != torch.int32
-                               or not status.is_contiguous() or status.device != nominal.device):
-        raise ValueError("status must be a contiguous int32 [units] device tensor")
-    s = stream if stream is not None else torch.cuda.current_stream(nominal.device)
-    _native.check(_native.lib().drcvar_sample_and_evaluate_f64(
-        ctypes.c_void_p(nominal.data_ptr()), O, T, nominal.stride(0), nominal.stride(1),
-        unit_begin, unit_count, n_samples, float(L[0, 0]), float(L[1, 0]), float(L[1, 1]),
-        ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), ctypes.c_uint64(int(stream_offset) & (2 ** 64 - 1)),
-        1 if zero_first_step else 0, ctypes.c_void_p(ego_units.data_ptr()), ego_units.stride(0),
-        params.robot_radius, params.obstacle_radius, params.alpha, params.delta, params.epsilon,
-        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr() if status is not None else 0),
-        ctypes.c_void_p(int(s.cuda_stream))))
-    return out
-
-
 def generate_obstacle_scenarios_device(scenario_config, horizon, dt, n_samples=100, seed=0,
                                        device=None):
     """``generate_obstacle_scenarios`` with the samples drawn on the device.

@@ -68,26 +68,6 @@ int drcvar_sample_units_f64(const double* nominal, int64_t n_obstacles, int64_t 
                             uint64_t stream_offset, int32_t zero_first_step, double* out,
                             int64_t su, int64_t sn, void* stream);
 
-/*
- * Draw + evaluate in one launch (round 4): units [unit_begin, unit_begin + unit_count) of the
- * global batch, drawn IN REGISTERS exactly as drcvar_sample_units_f64 draws them (same Philox
- * counters, same arithmetic: the samples are bit for bit the ones it would write) and evaluated as
- * drcvar_safe_halfspaces_f64_v2 evaluates a flat [unit_count, N, 2] block of them — the samples
- * never exist in memory.  Replaces, for device-sampled batches, the pair
- * simulation/obstacles.py:43-77 (the draw) -> core/halfspaces.py:196-248 (the evaluation).
- *   ego_units  [unit_count, 2] ego position per unit (stride ego_su between units)
- *   out        [unit_count, 8] records (DRCVAR_COL_*); status [unit_count] or NULL (DRCVAR_UNIT_*)
- * n_samples <= DRCVAR_MAX_SAMPLES (the register plans), else DRCVAR_ERR_UNSUPPORTED.
- */
-int drcvar_sample_and_evaluate_f64(const double* nominal, int64_t n_obstacles, int64_t n_steps,
-                                   int64_t nom_so, int64_t nom_st, int64_t unit_begin,
-                                   int64_t unit_count, int64_t n_samples, double l00, double l10,
-                                   double l11, uint64_t seed, uint64_t stream_offset,
-                                   int32_t zero_first_step, const double* ego_units,
-                                   int64_t ego_su, double robot_radius, double obstacle_radius,
-                                   double alpha, double delta, double epsilon, double* out,
-                                   int32_t* status, void* stream);
-
 #ifdef __cplusplus
 }
 #endif

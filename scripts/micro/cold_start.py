@@ -29,7 +29,7 @@ def graph_of(sb, n, dev):
     with torch.cuda.graph(g, stream=torch.cuda.Stream(dev)):
         launch = sb.prepare(torch.cuda.current_stream(dev))
         for _ in range(n):
-            launch()
+            sb.compute(launch)  # prepare() returns one frozen launch per chunk
     g.replay()
     torch.cuda.synchronize()
     return g, launch

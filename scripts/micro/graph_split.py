@@ -39,7 +39,7 @@ def main():
         with torch.cuda.graph(g, stream=torch.cuda.Stream(dev)):
             launch = sb.prepare(torch.cuda.current_stream(dev))
             for _ in range(n):
-                launch()
+                sb.compute(launch)  # prepare() returns one frozen launch per chunk
         g.replay()
         graphs[n] = (g, launch)
     torch.cuda.synchronize()

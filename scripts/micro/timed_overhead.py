@@ -45,7 +45,7 @@ def main():
             with torch.cuda.graph(g, stream=torch.cuda.Stream(dev)):
                 launch = sb.prepare(torch.cuda.current_stream(dev))
                 for _ in range(G):
-                    launch()
+                    sb.compute(launch)  # prepare() returns one frozen launch per chunk
             g.replay()
             torch.cuda.synchronize()
             graphs[G] = (g, launch)

@@ -270,3 +270,34 @@ def test_gpu_cluster_timeout_at_final_exchange_rolls_out_fallback(dev):
     assert ms < 5.0, f"timeout path took {ms:.3f} ms"
     # the surface wrapper reports it as a failed solve with the fallback (core/mpc_filter.py:168-173)
     assert mf.STATUS_NAMES[int(info[0, _native.MPC_INFO_STATUS])] not in mf.SOLVED
+
+
+@pytest.mark.gpu
+def test_gpu_retry_cluster_failures_patches_the_one_workgroup_optimum(dev, cluster_size):
+    """the device path of retry_cluster_failures.  Both problems of a clustered batch end
+    CLUSTER_TIMEOUT (options.debug_stall_group); the retry re-solves them on one workgroup each and
+    patches x / u / info in place through index_select / index_copy_ — the outputs must equal a
+    direct one-workgroup solve bit for bit and match the oracle."""
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    probs = _batch("double", 50, 256, 2, False, seed=17)
+    p0 = probs[0]
+    model = mf.MPCModel(p0["A"], p0["B"], p0["C"], p0["Q"], p0["R"], p0["H"], p0["ub"], p0["pb"],
+                        device=dev)
+    T_ = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    hs = T_(np.stack([p["hs"] for p in probs]))
+    args = (model, hs[..., 0:2], hs[..., 2], T_(np.stack([p["x0"] for p in probs])),
+            T_(np.stack([p["x_ref"] for p in probs])), T_(np.stack([p["u_ref"] for p in probs])))
+    x, u, info = mf.filter_batch(*args, options=mf.make_options(debug_stall_group=5, spin_limit_us=300))
+    status = info[:, _native.MPC_INFO_STATUS].cpu().numpy()
+    assert (status == _native.MPC_STATUS_CLUSTER_TIMEOUT).all(), status
+    with pytest.warns(RuntimeWarning, match="re-solving"):
+        retried = mf.retry_cluster_failures(*args, x, u, info)
+    assert retried == [0, 1]
+    x1, u1, info1, g1 = _solve(probs, dev, cluster_size(1))
+    assert g1 == 1
+    np.testing.assert_array_equal(u.cpu().numpy(), u1)
+    np.testing.assert_array_equal(x.cpu().numpy(), x1)
+    np.testing.assert_array_equal(info.cpu().numpy(), info1)
+    _check_vs_oracle(probs, x.cpu().numpy(), u.cpu().numpy(), info.cpu().numpy(), "retried")
+    assert mf.retry_cluster_failures(*args, x, u, info) == []  # nothing left to retry
