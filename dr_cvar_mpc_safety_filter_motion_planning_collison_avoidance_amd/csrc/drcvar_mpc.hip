@@ -59,7 +59,7 @@
 namespace drcvar_mpc_detail {
 
 struct BlobLayout {
-  int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, UF1, UF2, UFOK, total;
+  int64_t H0, F1, F2, Mp, CA, A, B, C, Q, R, UF1, UF2, UFOK, ISO, total;
 };
 
 inline BlobLayout blob_layout(int nx, int nu, int H) {
@@ -81,6 +81,9 @@ inline BlobLayout blob_layout(int nx, int nu, int H) {
   L.UF1 = o; o += n * nx;
   L.UF2 = o; o += n * H * nx;
   L.UFOK = o; o += 1;
+  // 1 for a planar isotropic model (nx = 4, nu = 2, A = [[a00 I, a01 I], [a10 I, a11 I]],
+  // B = [[b0 I], [b1 I]]: the reference's double integrator): the register-form factorisation
+  L.ISO = o; o += 1;
   L.total = o;
   return L;
 }
@@ -271,6 +274,7 @@ struct Lds {
   double* xs;     // [H+1][nx] rollout
   double* red;    // [kWaves][kPerStepQ][64] per-step partial sums
   double* sc;     // [64] block scalars
+  bool iso;       // planar isotropic model (blob ISO): riccati_factor_iso
 };
 
 // Fixed LDS plan per size class: every array sits at a compile-time offset, so LDS addresses are
@@ -331,9 +335,10 @@ static_assert(LdsPlan<2, 4, 4, kShortHorizon>::total * 8 <= 160 * 1024 / 3 &&
               "128-thread short-horizon plan: at least three workgroups per CU");
 
 template <int NW, int NU, int NX, int HMX>
-__device__ inline Lds carve(double* base) {
+__device__ inline Lds carve(double* base, bool iso) {
   using P = LdsPlan<NW, NU, NX, HMX>;
   Lds s;
+  s.iso = NU == 2 && NX == 4 && iso;
   s.Am = base + P::Am;
   s.Bm = base + P::Bm;
   s.Cm = base + P::Cm;
@@ -400,6 +405,37 @@ __device__ __forceinline__ double wave_butterfly(double v, F op) {
   }
   return v;
 }
+// Lane moves of the register-form factorisation (riccati_factor_iso): a DPP permutation within
+// rows of 16 lanes (two v_mov_b32_dpp), lane n of each row to the whole row (one v_mov_b64_dpp
+// row_newbcast, gfx950), and an arbitrary source lane (ds_bpermute: the LDS crossbar, ~75 cycles)
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int N>
+__device__ __forceinline__ double row_bcast_f64(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const long long y = __builtin_amdgcn_mov_dpp(x, 0x150 + N, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, y);
+}
+__device__ __forceinline__ double bperm_f64(double v, int byte_addr) {
+  const int lo = __builtin_amdgcn_ds_bpermute(byte_addr, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(byte_addr, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+// separately rounded product and sum (never contracted into an fma): the symmetric-exact sums of
+// riccati_factor_iso rely on a * b == b * a and a + b == b + a bit for bit
+__device__ __forceinline__ double mul_rn(double a, double b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ double add_rn(double a, double b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
 // The interior-point block sums keep the xor butterfly (distances 32, 16, ..., 1): the DPP tree
 // associates the sum differently, and that rounding was enough to turn one degenerate test
 // instance (generic1, H = 64, more binding rows than inputs) from a successful polish into an
@@ -714,11 +750,141 @@ __device__ __forceinline__ void prog_wait(const Lds& s, int q, int k) {
   wave_lds_fence();
 }
 
+
+// ---- Register-form factorisation of planar isotropic models (round 5) ----
+// For NX = 4, NU = 2 with A = [[a00 I, a01 I], [a10 I, a11 I]] and B = [[b0 I], [b1 I]] (the
+// reference's double integrator; blob ISO), the recursion runs on one wave with P in registers:
+// lane 4i + j (every row of 16 lanes alike) holds P_ij, and the step
+//   U = P B:     U_ic = b0 P_{i,c} + b1 P_{i,c+2}              (quad_perm within quad i)
+//   Re = Rb + B'U,  Ri = Re^-1                                  (U by row_newbcast: every lane alike)
+//   M = P - U Ri U':  M_ij from rows i (quad_perm) and j (ds_bpermute, issued early)
+//   P_k = Qb_k + A'M A = Qb_k + c00 M_ij + (c01 M_{i,j^2} + c10 M_{i^2,j}) + c11 M_{i^2,j^2}
+// couples a lane only with lanes l ^ 2, l ^ 8, l ^ 10 (quad_perm, row_ror:8), and with
+// c00 = a[bi][bi] a[bj][bj], c01 = a[bi][bi] a[1-bj][bj], c10 = a[1-bi][bi] a[bj][bj],
+// c11 = a[1-bi][bi] a[1-bj][bj] (i = 2 bi + xi), every product rounded separately and the middle
+// pair added first, the update is invariant under i <-> j bit for bit: P stays exactly symmetric
+// with no transpose (the LDS form forms the lower triangle and mirrors it).  No LDS round trip sits
+// on the chain: the step reads one record of a table built in front of the loop (the 10 canonical
+// entries of Qb_k and Rb_k's diagonal) and writes Ri_k, the gains Kg_k and the solve map F_k, the
+// last two formed off the chain from U_k (so riccati_maps has nothing left to do).  Measured on the bench's
+// model (scripts/micro/riccati_dpp.hip, one wave): ~500 cycles per step against 921 for the LDS
+// form, the same accuracy against a long-double recursion.  A failed pivot is not tested per step:
+// the minimum over the steps of det(Re) and Re00, and P_0 finite (a NaN or infinity anywhere
+// reaches it), give the same verdict at the end.
+// The table sits in s.red behind the pipelined solve's forward sources ([4 H]): records [H][12].
+__device__ __forceinline__ double* iso_qb(const Lds& s, int H) { return s.red + 4 * H; }
+__device__ __forceinline__ int iso_canon(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
+
+template <bool kPublish>
+__device__ __forceinline__ void riccati_factor_iso(const Lds& s, int H) {
+  const int lane = threadIdx.x & 63;
+  double* qbt = iso_qb(s, H);
+  // the table, lane = step: record k holds Qb_k = qb(k - 1) (record 0: the terminal qb(H - 1)) and
+  // Rb_k's diagonal; the entries as the LDS form sums them (2 Q_ab + C'S C, lower triangle)
+  for (int kk = lane; kk < H; kk += 64) {
+    const int rk = kk + 1 < H ? kk + 1 : 0;
+    const double S00 = s.S[kk], S01 = s.S[H + kk], S11 = s.S[2 * H + kk];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) {
+        const double c0a = s.Cm[a], c1a = s.Cm[kMx + a], c0b = s.Cm[b], c1b = s.Cm[kMx + b];
+        qbt[rk * 12 + iso_canon(a, b)] =
+            2.0 * s.Qm[a * kMx + b] + c0a * (S00 * c0b + S01 * c1b) + c1a * (S01 * c0b + S11 * c1b);
+      }
+    qbt[kk * 12 + 10] = 2.0 * s.Rm[0] + s.DU[kk * 2];
+    qbt[kk * 12 + 11] = 2.0 * s.Rm[3] + s.DU[kk * 2 + 1];
+  }
+  wave_lds_fence();
+  const int l = lane & 15, i = l >> 2, j = l & 3, bi = i >> 1, bj = j >> 1;
+  const int ia = i > j ? i : j, jb = i > j ? j : i;
+  const int qoff = iso_canon(ia, jb);
+  const double aa[2][2] = {{s.Am[0], s.Am[2]}, {s.Am[2 * kMx], s.Am[2 * kMx + 2]}};
+  const double b0 = s.Bm[0], b1 = s.Bm[2 * 2];
+  const double c00 = mul_rn(aa[bi][bi], aa[bj][bj]), c01 = mul_rn(aa[bi][bi], aa[1 - bj][bj]);
+  const double c10 = mul_rn(aa[1 - bi][bi], aa[bj][bj]), c11 = mul_rn(aa[1 - bi][bi], aa[1 - bj][bj]);
+  const double R01 = 2.0 * s.Rm[1];
+  const int src_j0 = ((lane & ~15) + 4 * j) * 4, src_j1 = src_j0 + 4;  // ds_bpermute byte addresses
+  const double* rec = qbt + (H - 1) * 12;
+  double p = qbt[qoff];  // the terminal Qb
+  double mn = 1.0;
+  // per step, off the chain: the gains Kg_k (lanes j < 2: Kg[k][u = j][x = i]) and the solve map
+  // F_k = A' - Kg_k' B' (lane 4i + j: F_k[i][j], every lane of the row of 16 a distinct entry), from
+  // L_{d,i} = (U'A)_{d,i} = alpha_i U_{i,d} + beta_i U_{i^2,d} (alpha_i = a[bi][bi], beta_i =
+  // a[1-bi][bi]; row i ^ 2 of U by row_ror:8); Ri_k by lane 0.  Lanes without a slot write the
+  // same instructions into scratch (s.P / s.T, unused by this form).
+  const double alpha = aa[bi][bi], beta = aa[1 - bi][bi];
+  const double Aji = s.Am[j * kMx + i], Bj0 = s.Bm[j * 2], Bj1 = s.Bm[j * 2 + 1];
+  double* kg_at = j < 2 ? s.Kg + (H - 1) * 8 + j * 4 + i : s.P + l;
+  const int kg_step = j < 2 ? 8 : 0;
+  double* sm_at = s.SM + (H - 1) * 16 + l;
+  double* ri_at = l == 0 ? s.Ri + (H - 1) * 4 : s.P + 16 + l;
+  const int ri_step = l == 0 ? 4 : 0;
+  for (int k = H - 1; k >= 0; --k) {
+    const double qn = rec[qoff];  // Qb_k (not used at k = 0)
+    const double rb00 = rec[10], rb11 = rec[11];
+    rec -= 12;
+    const double pa = dpp_mov_f64<0x44>(p), pb = dpp_mov_f64<0xEE>(p);  // quad_perm [0,1,0,1], [2,3,2,3]
+    const double uu = fma(b1, pb, b0 * pa);                                // U_{i, j & 1}
+    const double Ub0 = bperm_f64(uu, src_j0), Ub1 = bperm_f64(uu, src_j1);  // row j of U
+    __builtin_amdgcn_sched_barrier(0);  // both permutes issue here: their latency hides behind Re
+    const double U00 = row_bcast_f64<0>(uu), U01 = row_bcast_f64<1>(uu), U11 = row_bcast_f64<5>(uu);
+    const double U20 = row_bcast_f64<8>(uu), U21 = row_bcast_f64<9>(uu), U31 = row_bcast_f64<13>(uu);
+    const double Ua0 = dpp_mov_f64<0x00>(uu), Ua1 = dpp_mov_f64<0x55>(uu);  // row i of U
+    const double Re00 = fma(b1, U20, fma(b0, U00, rb00));
+    const double Re01 = fma(b1, U21, fma(b0, U01, R01));
+    const double Re11 = fma(b1, U31, fma(b0, U11, rb11));
+    const double det = fma(Re00, Re11, -(Re01 * Re01));
+    const double id = rcp(det);
+    mn = fmin(mn, fmin(det, Re00));
+    const double Ri00 = Re11 * id, Ri01 = -Re01 * id, Ri11 = Re00 * id;
+    ri_at[0] = Ri00;
+    ri_at[1] = Ri01;
+    ri_at[2] = Ri01;
+    ri_at[3] = Ri11;
+    ri_at -= ri_step;
+    {  // gains and solve map of step k
+      const double Uo0 = dpp_mov_f64<0x128>(Ua0), Uo1 = dpp_mov_f64<0x128>(Ua1);  // row i ^ 2
+      const double L0 = fma(beta, Uo0, alpha * Ua0), L1 = fma(beta, Uo1, alpha * Ua1);
+      const double K0 = fma(Ri01, L1, Ri00 * L0), K1 = fma(Ri11, L1, Ri01 * L0);
+      *kg_at = (j & 1) ? K1 : K0;
+      kg_at -= kg_step;
+      *sm_at = fma(-K1, Bj1, fma(-K0, Bj0, Aji));
+      sm_at -= 16;
+    }
+    if constexpr (kPublish) prog_publish(s, 0, k);  // Kg_k, Ri_k, F_k are out
+    const double m00 = mul_rn(Ua0, Ub0), m11 = mul_rn(Ua1, Ub1);
+    const double m01 = add_rn(mul_rn(Ua0, Ub1), mul_rn(Ua1, Ub0));
+    const double M = p - fma(m00, Ri00, fma(m01, Ri01, m11 * Ri11));
+    const double Mc = dpp_mov_f64<0x4E>(M);   // l ^ 2: quad_perm [2,3,0,1]
+    const double Mr = dpp_mov_f64<0x128>(M);  // l ^ 8: row_ror:8
+    const double Md = dpp_mov_f64<0x4E>(Mr);  // l ^ 10
+    const double t = add_rn(mul_rn(c01, Mc), mul_rn(c10, Mr));
+    p = qn + add_rn(add_rn(mul_rn(c00, M), t), mul_rn(c11, Md));
+  }
+  const bool ok = mn > 0.0 && __builtin_isfinite(p);
+  const bool all_ok = __ballot(!ok) == 0ull;  // uniform
+  if (lane == 0) {
+    s.sc[62] = all_ok ? 0.0 : 1.0;
+    s.sc[61] = 1.0;  // the solve maps are formed (riccati_maps has nothing to do)
+  }
+  if constexpr (kPublish) {
+    if (!all_ok) prog_publish(s, 0, kProgAbort);
+  }
+}
+
 template <int NU, int NX, bool kStationary = false, bool kPublish = false>
-__device__ inline void riccati_factor_wave0(const Lds& s, int H) {
+__device__ __forceinline__ void riccati_factor_wave0(const Lds& s, int H) {
   const int tid = threadIdx.x, lane = tid & 63;
   double* flag = s.sc + 62;
+  if constexpr (NU == 2 && NX == 4 && !kStationary) {
+    if (s.iso) {  // uniform
+      if (tid < 64) riccati_factor_iso<kPublish>(s, H);
+      return;
+    }
+  }
   if (tid < 64) {
+    if (lane == 0) s.sc[61] = 0.0;  // this form writes the gains itself
     constexpr int NX2 = NX * NX;
     const int e = lane < NX2 ? lane : 0;
     const int i = e / NX, j = e % NX;  // entry (i, j) owned by lane < NX2
@@ -871,9 +1037,10 @@ __device__ inline void riccati_factor_wave0(const Lds& s, int H) {
 // After a barrier behind riccati_factor_wave0: its outcome (uniform) and, for NX <= 4, the solve
 // maps.  Every thread calls it.
 template <int NU, int NX>
-__device__ inline bool riccati_maps(const Lds& s, int H, bool ok) {
+__device__ __forceinline__ bool riccati_maps(const Lds& s, int H, bool ok) {
   const int tid = threadIdx.x;
   if constexpr (NX <= 4) {
+    if (ok && s.sc[61] != 0.0) return ok;  // uniform: the isotropic form wrote the maps itself
     if (ok) {  // the solves' maps F_k = A' - Kg_k' B' (row-major [k][r][c] in s.SM), once per factor
       for (int e = tid; e < H * 16; e += static_cast<int>(blockDim.x)) {
         const int k = e >> 4, r = (e >> 2) & 3, c = e & 3;
@@ -888,12 +1055,12 @@ __device__ inline bool riccati_maps(const Lds& s, int H, bool ok) {
   return ok;
 }
 template <int NU, int NX>
-__device__ inline bool riccati_factor_finish(const Lds& s, int H) {
+__device__ __forceinline__ bool riccati_factor_finish(const Lds& s, int H) {
   return riccati_maps<NU, NX>(s, H, s.sc[62] == 0.0);  // uniform
 }
 
 template <int NU, int NX, bool kStationary = false>
-__device__ inline bool riccati_factor(const Lds& s, int H) {
+__device__ __forceinline__ bool riccati_factor(const Lds& s, int H) {
   riccati_factor_wave0<NU, NX, kStationary>(s, H);
   __syncthreads();
   return riccati_factor_finish<NU, NX>(s, H);
@@ -903,7 +1070,7 @@ __device__ inline bool riccati_factor(const Lds& s, int H) {
 // Vectors travel between lanes by readlane (lane m < NX holds entry m), so a step of either pass
 // has no LDS round trip on its critical path; the step's gains are loaded one step ahead.
 template <int NU, int NX>
-__device__ inline void riccati_solve(const Lds& s, int H, double* x) {
+__device__ __forceinline__ void riccati_solve(const Lds& s, int H, double* x) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid < 64) {
     const int li = lane < NX ? lane : 0;
@@ -1036,15 +1203,12 @@ __device__ inline void riccati_solve(const Lds& s, int H, double* x) {
 // reaches every lane of its quad by DPP quad broadcasts (no LDS on the chain) and the step's map
 // row is loaded one step ahead — ~H short steps per pass and four barriers per solve, instead of
 // the 2 ceil(log2 H) + 6 barrier-separated levels of the parallel scan this replaced.
-template <int CTRL>
-__device__ __forceinline__ double quad_bcast_f64(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
+// (the quad's four entries are those of lanes 0..3 in every row of 16 (the quads replicate each
+// other), so each reaches every lane by one v_mov_b64 row_newbcast instead of two 32-bit quad_perm
+// moves: the same bits, half the instructions on the recurrences' chains)
 __device__ __forceinline__ double affine4(double w, const double (&f)[4], double v) {
-  const double v0 = quad_bcast_f64<0x00>(v), v1 = quad_bcast_f64<0x55>(v);
-  const double v2 = quad_bcast_f64<0xAA>(v), v3 = quad_bcast_f64<0xFF>(v);
+  const double v0 = row_bcast_f64<0>(v), v1 = row_bcast_f64<1>(v);
+  const double v2 = row_bcast_f64<2>(v), v3 = row_bcast_f64<3>(v);
   return fma(f[0], v0, fma(f[1], v1, w)) + fma(f[2], v2, f[3] * v3);
 }
 
@@ -1084,8 +1248,46 @@ __device__ __forceinline__ void load_fwd(StepData& d, const double* M, const dou
 // sources B kff_k in s.red; dpp_forward runs the forward recurrence and writes du = kff - Kg x.
 // (The interior-point loop's affine solve runs the backward half beside the factorisation,
 // affine_backward_follow, and only the forward half after it.)
+// The parallel tail of the backward half, after the recurrence left p_k in s.SV: kff_k = -Re_k^-1
+// (B' p_{k+1} - b_k) into kff (may be b: in place), the forward sources B kff_k into s.red.  Ends
+// with a barrier.
 template <int NU, int kBlock>
-__device__ inline void dpp_backward(const Lds& s, int H, double* x, const double* z) {
+__device__ __forceinline__ void dpp_backward_tail(const Lds& s, int H, const double* b, double* kff_out) {
+  const int t = threadIdx.x;
+  const double* W = s.SV;
+  double* G = s.red;
+  for (int e = t; e < H * 4; e += kBlock) {
+    const int k = e >> 2, i = e & 3;
+    double ge[NU], kff[NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+      double acc = -b[k * NU + c];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc += s.Bm[m * NU + c] * W[(k + 1) * 4 + m];  // p_H = W[H]
+      ge[c] = acc;
+    }
+    double gi = 0.0;
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+      double acc = 0.0;
+#pragma unroll
+      for (int d = 0; d < NU; ++d) acc -= s.Ri[(k * NU + c) * NU + d] * ge[d];
+      kff[c] = acc;
+      gi += s.Bm[i * NU + c] * acc;
+    }
+    G[e] = gi;
+    wave_lds_fence();  // the step's four lanes share one wave: every b_k read precedes the writes
+    if (i < NU) {
+#pragma unroll
+      for (int c = 0; c < NU; ++c)
+        if (c == i) kff_out[k * NU + c] = kff[c];
+    }
+  }
+  __syncthreads();
+}
+
+template <int NU, int kBlock>
+__device__ __forceinline__ void dpp_backward(const Lds& s, int H, double* x, const double* z) {
   const int t = threadIdx.x;
   double* W = s.SV;   // [H + 1][4]: Kg_k' b_k (+ C'z_{k-1}), then p_k (backward pass)
   double* G = s.red;  // [H][4]: B kff_k
@@ -1122,41 +1324,13 @@ __device__ inline void dpp_backward(const Lds& s, int H, double* x, const double
     }
   }
   __syncthreads();
-  // kff_k = -Re_k^-1 (B' p_{k+1} - b_k) into x; the forward source B kff_k into G
-  for (int e = t; e < H * 4; e += kBlock) {
-    const int k = e >> 2, i = e & 3;
-    double ge[NU], kff[NU];
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      double acc = -x[k * NU + c];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc += s.Bm[m * NU + c] * W[(k + 1) * 4 + m];  // p_H = W[H]
-      ge[c] = acc;
-    }
-    double gi = 0.0;
-#pragma unroll
-    for (int c = 0; c < NU; ++c) {
-      double acc = 0.0;
-#pragma unroll
-      for (int d = 0; d < NU; ++d) acc -= s.Ri[(k * NU + c) * NU + d] * ge[d];
-      kff[c] = acc;
-      gi += s.Bm[i * NU + c] * acc;
-    }
-    G[e] = gi;
-    wave_lds_fence();  // the step's four lanes share one wave: every b_k read precedes the writes
-    if (i < NU) {
-#pragma unroll
-      for (int c = 0; c < NU; ++c)
-        if (c == i) x[k * NU + c] = kff[c];
-    }
-  }
-  __syncthreads();
+  dpp_backward_tail<NU, kBlock>(s, H, x, x);
 }
 
 // The forward half: x_{k+1} = F_k' x_k + B kff_k from x_0 = 0 (F_k in s.SM, B kff_k in s.red),
 // du_k = kff_k - Kg_k x_k into du (kff may be du), the positions into pos.  Ends with a barrier.
 template <int NU, int kBlock>
-__device__ inline void dpp_forward(const Lds& s, int H, const double* kff, double* du, double* pos,
+__device__ __forceinline__ void dpp_forward(const Lds& s, int H, const double* kff, double* du, double* pos,
                                    const double* c) {
   const int t = threadIdx.x;
   double* W = s.SV;   // [H + 1][4]: x_k
@@ -1202,7 +1376,7 @@ __device__ inline void dpp_forward(const Lds& s, int H, const double* kff, doubl
 }
 
 template <int NU, int kBlock>
-__device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c,
+__device__ __forceinline__ void riccati_solve_dpp(const Lds& s, int H, double* x, double* pos, const double* c,
                                          const double* z) {
   dpp_backward<NU, kBlock>(s, H, x, z);
   dpp_forward<NU, kBlock>(s, H, x, x, pos, c);
@@ -1212,7 +1386,7 @@ __device__ inline void riccati_solve_dpp(const Lds& s, int H, double* x, double*
 // wave-serial recursion otherwise (Gp' z summed first).  With pos: the positions of the solution as
 // well, pos = c + Gp x (c may be null).  Ends with a barrier.
 template <int NU, int NX, int kBlock, int HMX>
-__device__ inline void newton_solve(const Lds& s, int H, int n, double* x, double* pos = nullptr,
+__device__ __forceinline__ void newton_solve(const Lds& s, int H, int n, double* x, double* pos = nullptr,
                                     const double* c = nullptr, const double* z = nullptr) {
   if constexpr (NX <= 4) {
     riccati_solve_dpp<NU, kBlock>(s, H, x, pos, c, z);
@@ -1329,84 +1503,71 @@ __device__ inline double dual_residual_wave(const Lds& s, int H, int n, bool has
   return rdm;
 }
 
-// The backward half of the affine solve (dpp_backward with b = dua, z = za), run by one wave beside
-// the factorisation and one step behind it: step k waits for the factorisation's Kg_k / Ri_k
-// (progress word 0) and the dual-residual wave's b_k (word 1), then forms row i of the solve map
-// F_k = A' - Kg_k' B' (into s.SM for the later solves), p_k = F_k p_{k+1} + Kg_k' b_k + C'z_{k-1},
-// kff_k = -Re_k^-1 (B' p_{k+1} - b_k) (into kff) and the forward source B kff_k (into s.red).
-// ~40 instructions per step against the factorisation's ~900-cycle step, so after the
-// factorisation only the forward half is left (~7 k cycles of the affine solve's ~17 k).
+// The backward recurrence of the affine solve (dpp_backward with b = dua, z = za), run by one wave
+// beside the factorisation and behind it: p_k = F_k p_{k+1} + Kg_k' b_k + C'z_{k-1} into s.SV
+// (p_H = C'z_{H-1}), four steps per wait on the factorisation's progress word (their rows of F_k,
+// gains and sources loaded together), after the dual-residual wave's one publication of every b_k.
+// Only the chain runs here (~20 instructions a step); kff_k and the forward sources follow in
+// dpp_backward_tail after the barrier, then the forward half (round 5: the follower also formed
+// kff and the sources per step and, at ~760 cycles a step, was P1's last wave).  The isotropic
+// factorisation writes the rows of F_k itself; otherwise they are formed here from the gains and
+// stored for the later solves.  Lanes without a slot write into scratch (s.dp: free from the
+// previous update to this iteration's corrector solve; the dual-residual wave scribbles there too).
 template <int NU>
-__device__ inline void affine_backward_follow(const Lds& s, int H, const double* b, const double* z,
-                                              double* kff) {
+__device__ __forceinline__ void affine_backward_follow(const Lds& s, int H, const double* b, const double* z) {
   const int lane = threadIdx.x & 63, i = lane & 3;
   const bool keeper = lane < 4;
-  double acol[4], Bm[4][NU], brow[NU];
+  double* W = s.SV;
+  double* junk = s.dp + lane;
+  double acol[4], Bm[4][NU];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     acol[c] = s.Am[c * kMx + i];  // A[c][i]: row i of A'
 #pragma unroll
     for (int u = 0; u < NU; ++u) Bm[c][u] = s.Bm[c * NU + u];
   }
-#pragma unroll
-  for (int u = 0; u < NU; ++u) brow[u] = s.Bm[i * NU + u];
   const double c0 = s.Cm[i], c1 = s.Cm[kMx + i];
   double p = z ? c0 * z[2 * H - 2] + c1 * z[2 * H - 1] : 0.0;  // p_H = C'z_{H-1}
-  prog_wait(s, 1, -1);  // every b_k (the dual-residual wave publishes once, early)
-  for (int k = H - 1; k >= 0; --k) {
-    prog_wait(s, 0, k);
-    double kgi[NU], bk[NU], ri[NU][NU];
+  *(keeper ? W + H * 4 + i : junk) = p;
+  prog_wait(s, 1, -1);  // every b_k (the dual-residual wave publishes once)
+  for (int k0 = H - 1; k0 >= 0; k0 -= 4) {
+    prog_wait(s, 0, k0 >= 3 ? k0 - 3 : 0);  // steps k0 .. k0 - 3 are out
+    double f[4][4], w[4];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      kgi[u] = s.Kg[(k * NU + u) * 4 + i];
-      bk[u] = b[k * NU + u];
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 - q >= 0 ? k0 - q : 0;  // (steps below 0 are computed and discarded)
+      double kgi[NU], acc = 0.0;
 #pragma unroll
-      for (int v = 0; v < NU; ++v) ri[u][v] = s.Ri[(k * NU + u) * NU + v];
+      for (int u = 0; u < NU; ++u) {
+        kgi[u] = s.Kg[(k * NU + u) * 4 + i];
+        acc += kgi[u] * b[k * NU + u];
+      }
+      const int kz = k >= 1 ? 2 * k - 2 : 0;
+      if (z) acc += k >= 1 ? c0 * z[kz] + c1 * z[kz + 1] : 0.0;
+      w[q] = acc;
+      if (s.iso) {  // uniform
+#pragma unroll
+        for (int c = 0; c < 4; ++c) f[q][c] = s.SM[(k * 4 + i) * 4 + c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double fr = acol[c];
+#pragma unroll
+          for (int u = 0; u < NU; ++u) fr -= kgi[u] * Bm[c][u];
+          f[q][c] = fr;
+          *(keeper && k0 - q >= 0 ? s.SM + (k * 4 + i) * 4 + c : junk) = fr;
+        }
+      }
     }
-    const int kz = k >= 1 ? 2 * k - 2 : 0;  // C'z_{k-1} (k >= 1), loaded with the rest
-    const double zc = z ? c0 * z[kz] + c1 * z[kz + 1] : 0.0;
-    double fr[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double acc = acol[c];
-#pragma unroll
-      for (int u = 0; u < NU; ++u) acc -= kgi[u] * Bm[c][u];
-      fr[c] = acc;
+    for (int q = 0; q < 4; ++q) {
+      const double pn = affine4(w[q], f[q], p);
+      const bool in = k0 - q >= 0;
+      p = in ? pn : p;
+      *(keeper && in ? W + (k0 - q) * 4 + i : junk) = p;  // p_k
     }
-    if (keeper) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s.SM[(k * 4 + i) * 4 + c] = fr[c];
-    }
-    double w = 0.0;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) w += kgi[u] * bk[u];
-    w += k >= 1 ? zc : 0.0;
-    const double pv0 = quad_bcast_f64<0x00>(p), pv1 = quad_bcast_f64<0x55>(p);
-    const double pv2 = quad_bcast_f64<0xAA>(p), pv3 = quad_bcast_f64<0xFF>(p);  // p_{k+1}
-    double ge[NU], gi = 0.0, mine = 0.0;
-#pragma unroll
-    for (int v = 0; v < NU; ++v) ge[v] = Bm[0][v] * pv0 + Bm[1][v] * pv1 + Bm[2][v] * pv2 + Bm[3][v] * pv3 - bk[v];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      double acc = 0.0;
-#pragma unroll
-      for (int v = 0; v < NU; ++v) acc -= ri[u][v] * ge[v];
-      gi += brow[u] * acc;
-      mine = i == u ? acc : mine;
-    }
-    if (keeper) {
-      s.red[k * 4 + i] = gi;
-      if (i < NU) kff[k * NU + i] = mine;
-    }
-    p = fma(fr[0], pv0, fma(fr[1], pv1, w)) + fma(fr[2], pv2, fr[3] * pv3);
   }
 }
-
-// ---------------------------------------------------------------------------------------------
-// Row algebra.  An inequality row is G z + w = d with slack w >= 0 and dual lambda >= 0; for a
-// Newton step with complementarity target r_c the reduced quantities are
-//   D = lambda / w,  rho = D r_p + r_c / w,  dlambda = D (G dz) + rho,  dw = -r_p - G dz.
-// Affine step: r_c = -w lambda.  Corrector: r_c = -w lambda - dw_aff dlambda_aff + sigma mu.
 
 struct HsRow {
   double h0, h1, g, sv, wA, lA, wB, lB;
@@ -1754,7 +1915,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   const int n = a.n, H = a.H, K = a.K, O = a.O, nx = a.nx;
   const int o_lo = CL ? static_cast<int>((static_cast<int64_t>(O) * cid) / cl_size) : 0;
   const int o_hi = CL ? static_cast<int>((static_cast<int64_t>(O) * (cid + 1)) / cl_size) : O;
-  const Lds s = carve<kWaves, NU, NX, HMX>(lds_raw);
+  const Lds s = carve<kWaves, NU, NX, HMX>(lds_raw, a.blob[a.off.ISO] != 0.0);
+  static_assert(kWaves * kPerStepQ * 64 >= 16 * HMX, "s.red holds the isotropic factorisation's table");
   const double* H0 = a.blob + a.off.H0;
   double* ws = a.ws + a.ws_off + b * a.ws_pp;
   Cluster cl{};
@@ -2096,7 +2258,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         riccati_factor_wave0<NU, NX, false, NX <= 4 && kPipe>(s, H);
       } else if constexpr (NX <= 4) {
         if (wave == 1) rdm = fmax(rdm, dual_residual_wave<NU>(s, H, n, a.has_u, s.xs));
-        if (kPipe && wave == (kWaves >= 3 ? 2 : 1)) affine_backward_follow<NU>(s, H, s.dua, s.za, s.du);
+        if (kPipe && wave == (kWaves >= 3 ? 2 : 1)) affine_backward_follow<NU>(s, H, s.dua, s.za);
       } else {
         // (NX > 4 keeps the affine rhs's Gp' za in these rows: handing it to the solve as for
         // the other systems made the 4-input, 8-state kernels diverge on every problem of
@@ -2154,7 +2316,10 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     CL_NOTE(s.Ri[0]);  // the factorisation (its first pivot's inverse)
     MPC_PHASE(3);
     if constexpr (NX <= 4) {
-      if (piped) dpp_forward<NU, kBlock>(s, H, s.du, s.dua, s.dpa, nullptr);  // direction, positions
+      if (piped) {  // the backward recurrence ran beside the factorisation: its tail, the forward half
+        dpp_backward_tail<NU, kBlock>(s, H, s.dua, s.du);
+        dpp_forward<NU, kBlock>(s, H, s.du, s.dua, s.dpa, nullptr);  // direction, positions
+      }
       else newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.dua, s.dpa, nullptr, s.za);
     } else {  // (dua holds the whole rhs, Gp' za included)
       newton_solve<NU, NX, kBlock, HMX>(s, H, n, s.dua, s.dpa);
@@ -2422,6 +2587,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     bool done = false;
     if constexpr (NX <= 4 && kPipe) {
       if (s.sc[62] == 0.0) {  // uniform: the backward half ran beside the factorisation
+        dpp_backward_tail<NU, kBlock>(s, H, s.dua, s.du);
         dpp_forward<NU, kBlock>(s, H, s.du, s.dua, s.dpa, nullptr);  // affine du, dp
         predicted = done = true;
       }
@@ -3230,6 +3396,20 @@ int drcvar_mpc_model_init(const double* A, const double* B, const double* C, con
     }
     blob[L.UFOK] = ok ? 1.0 : 0.0;
   }
+  // a planar isotropic model (nx = 4, nu = 2, A = [[a00 I, a01 I], [a10 I, a11 I]], B = [[b0 I],
+  // [b1 I]]; the reference's double integrator) takes the register-form factorisation
+  // (riccati_factor_iso); exact comparisons: any other model keeps the general form
+  bool iso = nx == 4 && nu == 2;
+  for (int bi = 0; bi < 2 && iso; ++bi)
+    for (int bj = 0; bj < 2 && iso; ++bj) {
+      const double* a = A + 2 * bi * 4 + 2 * bj;  // block (bi, bj), row stride 4
+      iso = a[0] == a[5] && a[1] == 0.0 && a[4] == 0.0;
+    }
+  for (int bi = 0; bi < 2 && iso; ++bi) {
+    const double* b = B + 2 * bi * 2;  // rows 2 bi, 2 bi + 1 (row stride 2)
+    iso = b[0] == b[3] && b[1] == 0.0 && b[2] == 0.0;
+  }
+  blob[L.ISO] = iso ? 1.0 : 0.0;
   std::memcpy(blob + L.A, A, sizeof(double) * nx * nx);
   std::memcpy(blob + L.B, B, sizeof(double) * nx * nu);
   std::memcpy(blob + L.C, C, sizeof(double) * 2 * nx);

@@ -176,6 +176,9 @@ def test_model_init_condensation(dyn):
         o += want.size
     assert blob[o] == 1.0
     o += 1
+    # the planar isotropic flag (the double integrator: the register-form factorisation)
+    assert blob[o] == (1.0 if dyn == "double" else 0.0)
+    o += 1
     assert o == m.blob_doubles
 
 
