@@ -39,7 +39,7 @@ def busy_times(pmc_dir, kernel):
     for d, w in win.items():
         c = cnt[d]
         if c.get("GRBM_COUNT"):
-            out.append((w, w * c["GRBM_GUI_ACTIVE"] / c["GRBM_COUNT"]))
+            out.append((w, w * c["GRBM_GUI_ACTIVE"] / c["GRBM_COUNT"], c["GRBM_GUI_ACTIVE"] / c["GRBM_COUNT"]))
     return out
 
 
@@ -67,7 +67,10 @@ def main():
         "kernel": a.kernel, "command": a.command, "source_key": _native.source_key(),
         "busy": {"file": a.pmc_file, "dispatches": len(b), "mean_ns": statistics.fmean(x[1] for x in b),
                  "median_ns": statistics.median(x[1] for x in b), "window_mean_ns": statistics.fmean(x[0] for x in b),
-                 "method": "per dispatch: (End - Start) x GRBM_GUI_ACTIVE / GRBM_COUNT of a --pmc pass"},
+                 "gui_active_over_count_mean": statistics.fmean(x[2] for x in b),
+                 "method": ("per dispatch of a --pmc pass (dispatches serialised, none overlapped by the "
+                            "profiler's completion handling of graph replays): (End - Start) x "
+                            "GRBM_GUI_ACTIVE / GRBM_COUNT; a ratio of 1 makes it the dispatch window")},
         "trace": {"file": a.trace_file, "dispatches": len(t), "mean_ns": statistics.fmean(t),
                   "median_ns": statistics.median(t), "min_ns": min(t),
                   "method": "rocprofv3 --kernel-trace dispatch windows (stretched by the profiler)"}}
