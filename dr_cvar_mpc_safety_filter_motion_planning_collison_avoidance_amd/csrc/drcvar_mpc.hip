@@ -157,6 +157,14 @@ constexpr double kPolishRho = DRCVAR_POLISH_RHO;    // method-of-multipliers pen
 constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
+// early polish (round 5): a first round whose merit is <= kEarlyPolishMerit but fell less than
+// tenfold over the last two iterations is stalled by weakly active rows (w and lambda of a pair
+// both heading to zero: the Mehrotra steps alternate long and short; the straggler of
+// tests/golden/qp_h30_straggler.npz took 20 iterations against a batch mean of 5.3), so it
+// polishes from there; a polish that fails resumes the interior-point method to the tolerance
+constexpr double kEarlyPolishMerit = 1e-3;
+constexpr double kStallRatio = 0.1;
+constexpr int kEarlyPolishAttempts = 2;  // active-set corrections of an early polish
 constexpr double kPolishDualTol = 1e-7;
 constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
 constexpr double kStartMuMany = 20.0;   // barrier parameter of the starting point, >= 64 obstacles
@@ -2165,6 +2173,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // one round: P1 of the current iterate, the interior-point loop, the polish; true when a resume
   // round should follow.  Inlined at both call sites (a loop around it, or an out-of-line
   // function, made the compiler spill inside the interior-point loop: C5 QP +5 % / +40 %).
+  double merit_back1 = kHuge, merit_back2 = kHuge;  // the merit one and two iterations back
+  bool early = false;  // the first round left for an early polish (kEarlyPolishMerit)
   auto ipm_round = [&](const int round) __attribute__((always_inline)) -> bool {
   bool converged = false;  // this round's loop met its tolerance (the factorisation beside it stands)
   // positions of the starting (or restored) iterate and its P1 row pass
@@ -2290,6 +2300,14 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         best_merit = merit;
         break;
       }
+      if (round == 0 && a.polish && merit <= kEarlyPolishMerit && merit > kStallRatio * merit_back2) {
+        converged = true;  // (the factorisation beside this P1 serves the active-set guess)
+        early = true;
+        best_merit = merit;
+        break;
+      }
+      merit_back2 = merit_back1;
+      merit_back1 = merit;
       if (merit < best_merit) {  // uniform: every thread holds the same merit
         best_merit = merit;
         best_it = it;
@@ -2570,7 +2588,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // reuse the Hessian assembly, the Cholesky and the triangular solves), and rows whose sign
   // conditions fail are moved (primal-dual active-set step), up to kPolishAttempts times.  On
   // success the answer is exact to roundoff; otherwise the interior-point answer stands.
-  const bool tried = a.polish && best_merit <= kPolishMerit && !(CL && cl.aborted);
+  const bool tried = a.polish && (best_merit <= kPolishMerit || (early && round == 0)) && !(CL && cl.aborted);
   // The active-set guess from the predictor (round 5).  On the iteration that met the tolerance
   // wave 0 has factorised the Newton matrix beside the affine rhs (s.dua), so one solve gives the
   // affine direction at the endpoint, and every complementary pair (w, lambda) is classified by
@@ -2665,6 +2683,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       // test hook; a loop bound computed from it instead (attempts = hook ? 0 : kPolishAttempts)
       // broke the 4-input kernels' polish (8 % polished) — a codegen effect, not a semantic one
       if (round == 0 && a.force_resume) break;
+      if (round == 0 && early && attempt >= kEarlyPolishAttempts) break;  // (a break: see above)
       ++polish_attempts;
       // Hessian of the active-set problem: 100 h h' for positive slacks, rho h h' for equalities
       {
@@ -2956,7 +2975,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     }
     __syncthreads();
   }
-  bool resume = round == 0 && tried && !polished && status == DRCVAR_MPC_STATUS_OPTIMAL && it < a.max_iter;
+  bool resume = round == 0 && tried && !polished && (status == DRCVAR_MPC_STATUS_OPTIMAL || early) &&
+                it < a.max_iter;
   if constexpr (CL) resume = resume && !cl.aborted;
   if (!resume) return false;
   // restore what the polish overwrote (u is back already): the rows' s / w_hs and the bound states
@@ -2975,8 +2995,10 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     for (int k = 0; k < 4; ++k) s.px[k * 2 * H + t] = SAVED_B[4 * n + k * 2 * H + t];
   __syncthreads();
   status = DRCVAR_MPC_STATUS_MAX_ITER;
-  tol_r = a.tol * kResumeTol;
-  it_end = it + kResumeIters < a.max_iter ? it + kResumeIters : a.max_iter;
+  // after a failed early polish the method simply goes on to its tolerance; after a failed polish
+  // at the tolerance, a few more iterations towards a tighter one
+  tol_r = early ? a.tol : a.tol * kResumeTol;
+  it_end = early ? a.max_iter : (it + kResumeIters < a.max_iter ? it + kResumeIters : a.max_iter);
   return true;
   };  // ipm_round
   if (ipm_round(0)) ipm_round(1);

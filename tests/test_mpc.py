@@ -114,6 +114,27 @@ def test_oracle_polishes_the_degenerate_c5_handoff():
     assert abs(info["objective"] - float(z["objective"])) <= 1e-12 * float(z["objective"])
 
 
+def _h30_straggler():
+    z = load(os.path.join(GOLDEN_DIR, "qp_h30_straggler.npz"))
+    rows = [np.concatenate([z["h"][:, t], z["g"][:, t, None]], -1) for t in range(z["h"].shape[1])]
+    return z, rows
+
+
+def test_oracle_certifies_the_h30_straggler():
+    """The slowest of scripts/mpc_bench.py's 1024 distinct main.py-like QPs (tests/golden/
+    make_golden_qp_straggler.py: weakly active rows, the kernel's Mehrotra steps alternate long and
+    short): the oracle's answer is KKT-certified and reproduces the fixture."""
+    z, rows = _h30_straggler()
+    A, B, C = double_integrator()
+    H = z["x_ref"].shape[0] - 1
+    x, u, info = mpc_qp.filter_trajectory(A, B, C, 2 * np.eye(4), np.eye(2), H, z["x0"], z["x_ref"],
+                                          None, rows, tuple(z["u_bounds"]), tuple(z["p_bounds"]))
+    assert info["status"] == "optimal"
+    assert max(info["kkt"].values()) < 1e-9, info["kkt"]
+    np.testing.assert_allclose(u, z["u_expected"], atol=1e-9)
+    assert abs(info["objective"] - float(z["objective"])) <= 1e-12 * float(z["objective"])
+
+
 def test_oracle_without_constraints_is_the_lq_tracking_solution():
     A, B, C = double_integrator()
     H = 12
@@ -579,3 +600,28 @@ def test_gpu_degenerate_c5_handoff_matches_polished_oracle(dev):
         np.testing.assert_allclose(u[0].cpu().numpy(), z["u_expected"], atol=MPC_TOL)
         np.testing.assert_allclose(x[0].cpu().numpy(), z["x_expected"], atol=MPC_TOL)
         assert abs(info[_native.MPC_INFO_OBJECTIVE] - float(z["objective"])) <= 1e-9 * float(z["objective"])
+
+
+@pytest.mark.gpu
+def test_gpu_h30_straggler_matches_oracle(dev):
+    """The batch straggler (tests/golden/qp_h30_straggler.npz) alone and inside a 64-problem batch
+    of itself (the 128-thread form): polished, within MPC_TOL of the oracle's KKT-certified answer,
+    objective to 1e-9, and no more interior-point iterations than the dump recorded."""
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    z, _ = _h30_straggler()
+    A, B, C = double_integrator()
+    H = z["x_ref"].shape[0] - 1
+    model = mf.MPCModel(A, B, C, 2 * np.eye(4), np.eye(2), H, tuple(z["u_bounds"]), tuple(z["p_bounds"]),
+                        device=dev)
+    Tt = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    for Bn in (1, 160):  # 160 > kFewProblems: the batched (many-problem) kernel form
+        rep = lambda a: Tt(np.repeat(a[None], Bn, axis=0))
+        x, u, info = mf.filter_batch(model, rep(z["h"]), rep(z["g"]), rep(z["x0"]), rep(z["x_ref"]),
+                                     Tt(np.zeros((Bn, H, 2))))
+        info = info.cpu().numpy()
+        assert (info[:, _native.MPC_INFO_STATUS] == _native.MPC_STATUS_OPTIMAL).all(), info[0]
+        assert (info[:, _native.MPC_INFO_POLISHED] == 1).all(), info[0]
+        assert (info[:, _native.MPC_INFO_ITERATIONS] <= float(z["kernel_iterations"])).all(), info[0]
+        np.testing.assert_allclose(u.cpu().numpy(), np.repeat(z["u_expected"][None], Bn, 0), atol=MPC_TOL)
+        assert np.all(np.abs(info[:, _native.MPC_INFO_OBJECTIVE] - float(z["objective"])) <= 1e-9 * float(z["objective"]))
