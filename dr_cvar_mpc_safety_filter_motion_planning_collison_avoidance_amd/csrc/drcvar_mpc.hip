@@ -1473,12 +1473,39 @@ __device__ inline double dual_residual_wave(const Lds& s, int H, int n, bool has
     Src[e] = y;  // (Src's B u_k are no longer needed; y_k lands in Src, lambda_k in Xs)
   }
   wave_lds_fence();
-  {  // backward: lambda_k = y_k + A' lambda_{k+1}, lambda_{H+1} = 0
-    double lam = 0.0, y[4];
+  // the inputs' terms without lambda: f + 2 R u into s.rdu, the box duals' difference into s.dua;
+  // the backward chain adds B'lambda_{j+1} as soon as it has lambda_{j+1}, then the box term (the
+  // order of the earlier all-at-once form: a different rounding of r_du moved one degenerate batch
+  // problem from one polish attempt to six)
+  for (int j = lane; j < n; j += 64) {
+    const int jj = j / NU, ai = j - jj * NU;
+    double ru = 0.0;
+#pragma unroll
+    for (int c = 0; c < NU; ++c) ru += s.Rm[ai * NU + c] * s.u[jj * NU + c];
+    s.rdu[j] = s.f[j] + 2.0 * ru;
+    s.dua[j] = has_u ? s.bx[n + j] - s.bx[3 * n + j] : 0.0;
+  }
+  wave_lds_fence();
+  // backward: lambda_k = y_k + A' lambda_{k+1}, lambda_{H+1} = 0; at each k the input step k - 1's
+  // dual residual r_du = base + B'lambda_k and affine rhs dua = -r_du - rU (lanes c < NU), published
+  // every four steps (progress word 1 = the lowest input step out), so that the pipelined backward
+  // solve starts behind this chain instead of after all of it
+  const bool rkeeper = lane < NU;
+  const int cc = i < NU ? i : 0;
+  double bcol[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) bcol[m] = s.Bm[m * NU + cc];
+  double rdm = 0.0;
+  {
+    double lam = 0.0, y[4], base[4], box[4], ru[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int kk = H - q;
       y[q] = Src[(kk >= 1 ? kk : 1) * 4 + i];
+      const int jb = (kk >= 1 ? kk - 1 : 0) * NU + cc;
+      base[q] = s.rdu[jb];
+      box[q] = s.dua[jb];
+      ru[q] = s.rU[jb];
     }
     for (int k = H; k >= H + 1 - Hp; k -= 4) {
 #pragma unroll
@@ -1487,25 +1514,24 @@ __device__ inline double dual_residual_wave(const Lds& s, int H, int n, bool has
         const double ln = affine4(y[q], acol, lam);
         lam = kk >= 1 ? ln : lam;
         *(keeper && kk >= 1 ? Xs + kk * 4 + i : junk) = lam;  // lambda_kk
+        const double l0 = row_bcast_f64<0>(lam), l1 = row_bcast_f64<1>(lam);
+        const double l2 = row_bcast_f64<2>(lam), l3 = row_bcast_f64<3>(lam);
+        const double r = fma(bcol[3], l3, fma(bcol[2], l2, fma(bcol[1], l1, fma(bcol[0], l0, base[q])))) + box[q];
+        const bool out = rkeeper && kk >= 1;
+        const int jo = (kk - 1) * NU + i;
+        *(out ? s.rdu + jo : junk) = r;
+        *(out ? s.dua + jo : junk) = -r - ru[q];
+        rdm = out ? fmax(rdm, fabs(r)) : rdm;
         const int kn = kk - 4;
         y[q] = Src[(kn >= 1 ? kn : 1) * 4 + i];
+        const int jn = (kn >= 1 ? kn - 1 : 0) * NU + cc;
+        base[q] = s.rdu[jn];
+        box[q] = s.dua[jn];
+        ru[q] = s.rU[jn];
       }
+      const int lowest = k - 4;  // input steps >= lowest are out (k - 3 - 1)
+      prog_publish(s, 1, lowest > 0 ? lowest : 0);
     }
-  }
-  wave_lds_fence();
-  double rdm = 0.0;
-  for (int j = lane; j < n; j += 64) {
-    const int jj = j / NU, ai = j - jj * NU;
-    double ru = 0.0;
-#pragma unroll
-    for (int c = 0; c < NU; ++c) ru += s.Rm[ai * NU + c] * s.u[jj * NU + c];
-    double r = s.f[j] + 2.0 * ru;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) r += s.Bm[m * NU + ai] * Xs[(jj + 1) * 4 + m];
-    if (has_u) r += s.bx[n + j] - s.bx[3 * n + j];
-    s.rdu[j] = r;
-    rdm = fmax(rdm, fabs(r));
-    s.dua[j] = -r - s.rU[j];
   }
   prog_publish(s, 1, -1);  // every input step's rows are out
   return rdm;
@@ -1514,7 +1540,8 @@ __device__ inline double dual_residual_wave(const Lds& s, int H, int n, bool has
 // The backward recurrence of the affine solve (dpp_backward with b = dua, z = za), run by one wave
 // beside the factorisation and behind it: p_k = F_k p_{k+1} + Kg_k' b_k + C'z_{k-1} into s.SV
 // (p_H = C'z_{H-1}), four steps per wait on the factorisation's progress word (their rows of F_k,
-// gains and sources loaded together), after the dual-residual wave's one publication of every b_k.
+// gains and sources loaded together), each block as soon as the dual-residual wave's backward chain
+// has published its b_k.
 // Only the chain runs here (~20 instructions a step); kff_k and the forward sources follow in
 // dpp_backward_tail after the barrier, then the forward half (round 5: the follower also formed
 // kff and the sources per step and, at ~760 cycles a step, was P1's last wave).  The isotropic
@@ -1537,9 +1564,9 @@ __device__ __forceinline__ void affine_backward_follow(const Lds& s, int H, cons
   const double c0 = s.Cm[i], c1 = s.Cm[kMx + i];
   double p = z ? c0 * z[2 * H - 2] + c1 * z[2 * H - 1] : 0.0;  // p_H = C'z_{H-1}
   *(keeper ? W + H * 4 + i : junk) = p;
-  prog_wait(s, 1, -1);  // every b_k (the dual-residual wave publishes once)
   for (int k0 = H - 1; k0 >= 0; k0 -= 4) {
-    prog_wait(s, 0, k0 >= 3 ? k0 - 3 : 0);  // steps k0 .. k0 - 3 are out
+    prog_wait(s, 1, k0 >= 3 ? k0 - 3 : 0);  // b_k of steps k0 .. k0 - 3 (the dual-residual wave)
+    prog_wait(s, 0, k0 >= 3 ? k0 - 3 : 0);  // their gains and maps (the factorisation)
     double f[4][4], w[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1985,7 +2012,11 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // moved the rounding of f enough to stall one degenerate test problem (generic1, H = 64) at
   // merit 1e-8 with a failing polish (degenerate active sets defeat the polish)
   // (the row of F2 is loaded 16 doubles at a time, all in flight, ahead of the chain: one thread
-  // per row, so the row's ~H nx loads used to sit on the dependent chain one round trip at a time)
+  // per row, so the row's ~H nx loads used to sit on the dependent chain one round trip at a time).
+  // (Round 5 measured f through the dynamics on one wave for the isotropic models -- 2 Gx'Q (Phi x0
+  // - xr) by the free response and its adjoint, two H-step recurrences: C5 setup 47 k -> 21 k
+  // cycles but 99 k -> 90 k in all, and its rounding sent one degenerate problem of bench.py's
+  // distinct batch from one polish attempt to ten; not kept.)
   for (int j = tid; j < n; j += kBlock) {
     const double* f1 = a.blob + a.off.F1 + static_cast<int64_t>(j) * nx;
     const double* f2 = a.blob + a.off.F2 + static_cast<int64_t>(j) * H * nx;
