@@ -134,16 +134,30 @@ def _compile_units():
     return units
 
 
+def _quoted_includes(path: str, seen=None) -> list:
+    """The files a source pulls in through ``#include "..."`` (include/ or csrc/), transitively."""
+    import re
+    seen = set() if seen is None else seen
+    out = []
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', open(path).read(), re.M):
+        for d in (INCLUDE_DIR, os.path.join(PKG_DIR, "csrc")):
+            f = os.path.join(d, name)
+            if os.path.exists(f) and f not in seen:
+                seen.add(f)
+                out.append(f)
+                out.extend(_quoted_includes(f, seen))
+                break
+    return out
+
+
 def source_key(basename: str = "drcvar_halfspace.hip") -> str:
-    """A hash of one translation unit's inputs (its source, every header and .inc table it can
-    include, its extra compile flags): profiles/ evidence is tied to the kernel code it measured,
+    """A hash of one translation unit's inputs (its source, the headers and .inc tables it
+    includes, its extra compile flags): profiles/ evidence is tied to the kernel code it measured,
     and bench.py uses it only while the sources still match."""
-    import glob
     import hashlib
     src = os.path.join(PKG_DIR, "csrc", basename)
-    incs = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.inc")))
     h = hashlib.sha256(open(src, "rb").read())
-    for f in HEADERS + incs:
+    for f in _quoted_includes(src):
         h.update(open(f, "rb").read())
     for s, defs in _compile_units():
         if s == src:

@@ -154,13 +154,15 @@ int32_t drcvar_mpc_launch_groups_ex(const drcvar_mpc_model* model, int64_t n_pro
  *                           [n_obstacles, 64] arrays h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
  *                           (s = the slack of each halfspace at exit) and two saved across a failed
  *                           polish, then per workgroup the best iterate and the saved bound states
- *   max_iter, tol           interior-point limits (e.g. 60, 1e-8); converged when
+ *   max_iter, tol           interior-point limits (e.g. 60, 1e-7); converged when
  *                           max(|r_primal|/(1+|d|), |r_dual|/(1+|q|), mean complementarity) <= tol
  *   polish                  nonzero: finish with the active-set polish (method of multipliers on
  *                           the equality QP of the identified active set, with active-set
  *                           corrections) — exact to roundoff when it succeeds, as OSQP's polish;
  *                           when it fails on a problem that met tol, the interior-point method
- *                           resumes for up to 8 iterations towards tol * 1e-3 and polishes again
+ *                           resumes for up to 8 iterations towards tol * 1e-3 and polishes again;
+ *                           a first round stalled at merit <= 1e-3 polishes early (two corrections)
+ *                           and, when that fails, resumes towards tol
  */
 int drcvar_mpc_filter_f64(const drcvar_mpc_model* model, const double* blob, int64_t n_problems,
                           const double* hs_h, const double* hs_g, int64_t n_obstacles,
