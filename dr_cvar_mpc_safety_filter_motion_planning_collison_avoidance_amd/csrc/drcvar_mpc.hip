@@ -1937,7 +1937,7 @@ constexpr int kSweep = 1;
 // workgroups per CU, 128 threads with four.
 // CL: clustered form — a.cl_size workgroups per problem (grid = problems x cl_size), each
 // sweeping the obstacles [o_lo, o_hi) and exchanging row sums (cluster_combine).
-template <int NU, int NX, int BLK, int HMX, bool CL = false>
+template <int NU, int NX, int BLK, int HMX, bool CL = false, bool RL = false>
 __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kernel(MpcArgs a) {
   constexpr int kBlock = BLK;
   constexpr int kWaves = BLK / 64;
@@ -1974,8 +1974,17 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
 #endif
   // rows: [O][8 fields][64 steps] — one base, the field is an immediate offset
-  const RowArrays rows{ws, ws + kStepPad, ws + 2 * kStepPad, ws + 3 * kStepPad,
-                       ws + 4 * kStepPad, ws + 5 * kStepPad, ws + 6 * kStepPad, ws + 7 * kStepPad};
+  // The clustered form keeps its slice of the rows in LDS when the launch found room for it
+  // (the C5 hand-off: 16 obstacles x kRowStride doubles = 80 KB beside the 78 KB plan, one
+  // workgroup per CU): the row sweeps then wait on LDS instead of L2 (round 5); the layout and
+  // the arithmetic are the workspace's, indexed by the same r (the base is offset by o_lo).
+  // (RL: a kernel form of its own, so that the row accesses compile to LDS instructions)
+  double* rbase = ws;
+  if constexpr (CL && RL) {
+    rbase = lds_raw + (LdsPlan<kWaves, NU, NX, HMX>::total + kClusterScratch) - static_cast<int64_t>(o_lo) * kRowStride;
+  }
+  const RowArrays rows{rbase, rbase + kStepPad, rbase + 2 * kStepPad, rbase + 3 * kStepPad,
+                       rbase + 4 * kStepPad, rbase + 5 * kStepPad, rbase + 6 * kStepPad, rbase + 7 * kStepPad};
   const int64_t pitch = static_cast<int64_t>(O) * kStepPad;
   const double* x0 = a.x0 + b * a.x0_sp;
   const double* xr = a.xr + b * a.xr_sp;
@@ -2197,8 +2206,8 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   bool polished = false;
   // saved across a failed polish: the rows' s and w_hs (fields 8, 9 of every obstacle block) and
   // the bound states bx [4 n], px [8 H] (behind the best iterate)
-#define SAVED_S (ws + 8 * kStepPad)
-#define SAVED_W (ws + 9 * kStepPad)
+#define SAVED_S (rbase + 8 * kStepPad)
+#define SAVED_W (rbase + 9 * kStepPad)
 #define SAVED_B (ws + kRowArrays * pitch + static_cast<int64_t>(cid) * kBestPad + 128)
   it = 1;
   // one round: P1 of the current iterate, the interior-point loop, the polish; true when a resume
@@ -3157,18 +3166,17 @@ __global__ void zero_counters_kernel(double* ws, int n_problems) {
     __hip_atomic_store((gu64*)(ws + b * kCtrlDoubles), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NU, int NX, int BLK, int HMX = DRCVAR_MPC_MAX_HORIZON, bool CL = false>
-int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
-  // the clustered form asks for more LDS than two workgroups can share: one workgroup per CU
-  constexpr size_t plan_bytes = sizeof(double) * (LdsPlan<BLK / 64, NU, NX, HMX>::total + (CL ? kClusterScratch : 0));
-  constexpr size_t lds_bytes = CL && plan_bytes < 96 * 1024 ? 96 * 1024 : plan_bytes;
-  static bool attr_set = false;  // idempotent; a racing second call sets the same value
-  if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK, HMX, CL>),
+template <int NU, int NX, int BLK, int HMX, bool CL, bool RL>
+int launch_form(const MpcArgs& args, int64_t n_problems, size_t lds_req, size_t attr_bytes, hipStream_t stream) {
+  static bool attr_set[64] = {};  // per device; idempotent (a racing second call sets the same value)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return DRCVAR_ERR_LAUNCH;
+  if (!attr_set[dev]) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK, HMX, CL, RL>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(lds_bytes)) != hipSuccess)
+                            static_cast<int>(attr_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
-    attr_set = true;
+    attr_set[dev] = true;
   }
   // the arrival counters, zeroed in front of every launch by a one-wave kernel of agent-scope
   // (write-through) stores: a hipMemsetAsync node replayed from a hipGraph left the counters
@@ -3176,10 +3184,27 @@ int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
   // kernel every replay reproduced the eager launch, scripts/micro/cluster_graph_diag.py)
   if constexpr (CL)
     hipLaunchKernelGGL(zero_counters_kernel, dim3(1), dim3(64), 0, stream, args.ws, static_cast<int>(n_problems));
-  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK, HMX, CL>),
+  hipLaunchKernelGGL((mpc_ipm_kernel<NU, NX, BLK, HMX, CL, RL>),
                      dim3(static_cast<unsigned>(n_problems * (CL ? args.cl_size : 1))), dim3(BLK),
-                     lds_bytes, stream, args);
+                     lds_req, stream, args);
   return DRCVAR_OK;
+}
+
+template <int NU, int NX, int BLK, int HMX = DRCVAR_MPC_MAX_HORIZON, bool CL = false>
+int launch(const MpcArgs& args, int64_t n_problems, hipStream_t stream) {
+  // the clustered form asks for more LDS than two workgroups can share: one workgroup per CU
+  constexpr size_t plan_bytes = sizeof(double) * (LdsPlan<BLK / 64, NU, NX, HMX>::total + (CL ? kClusterScratch : 0));
+  constexpr size_t lds_bytes = CL && plan_bytes < 96 * 1024 ? 96 * 1024 : plan_bytes;
+  if constexpr (CL && NX <= 4) {
+    // the largest obstacle slice's rows in LDS beside the plan, when they fit (the C5 hand-off:
+    // 16 obstacles, 80 KB beside 78 KB): the RL form
+    constexpr size_t kLdsMax = 160 * 1024;  // gfx950: LDS per workgroup
+    const int64_t slice = (static_cast<int64_t>(args.O) + args.cl_size - 1) / args.cl_size;
+    const size_t rows_bytes = sizeof(double) * static_cast<size_t>(slice) * kRowStride;
+    if (plan_bytes + rows_bytes <= kLdsMax)
+      return launch_form<NU, NX, BLK, HMX, CL, true>(args, n_problems, plan_bytes + rows_bytes, kLdsMax, stream);
+  }
+  return launch_form<NU, NX, BLK, HMX, CL, false>(args, n_problems, lds_bytes, lds_bytes, stream);
 }
 
 template <int NU>
