@@ -111,6 +111,8 @@ def roofline_line(abytes, kernel_s, ktiming, traffic, args, step_s):
     command = f"python3 bench.py --gpus {args.gpus} --steps {args.steps} --warmup {args.warmup}"
     if args.workload != "c3" or args.launch != "graph":
         command += f" --workload {args.workload} --launch {args.launch}"
+    if args.lib:  # another library than the in-tree build: never the profiled one
+        command += f" --lib {args.lib}"
     ev = roofline(abytes, kernel_s, traffic)
     evidence, why = kernel_evidence(args.workload, abytes, command)
     if evidence is not None and evidence["busy"]["kernel_ms"] * 1e-3 <= step_s:
