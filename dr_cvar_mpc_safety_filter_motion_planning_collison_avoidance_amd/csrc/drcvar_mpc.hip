@@ -1567,28 +1567,46 @@ __device__ __forceinline__ void affine_backward_follow(const Lds& s, int H, cons
   for (int k0 = H - 1; k0 >= 0; k0 -= 4) {
     prog_wait(s, 1, k0 >= 3 ? k0 - 3 : 0);  // b_k of steps k0 .. k0 - 3 (the dual-residual wave)
     prog_wait(s, 0, k0 >= 3 ? k0 - 3 : 0);  // their gains and maps (the factorisation)
-    double f[4][4], w[4];
+    // every load of the block first, at clamped indices (steps below 0 are computed and
+    // discarded), so that they are in flight together: a per-step branch on the state source
+    // (k >= 1) had put a wait for each step's loads in front of the next step's
+    double f[4][4], w[4], kg[4][NU], bk[4][NU], zk[4][2];
+    const double* zp = z ? z : b;  // (read and not used without z)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int k = k0 - q >= 0 ? k0 - q : 0;  // (steps below 0 are computed and discarded)
-      double kgi[NU], acc = 0.0;
+      const int k = k0 - q >= 0 ? k0 - q : 0;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
-        kgi[u] = s.Kg[(k * NU + u) * 4 + i];
-        acc += kgi[u] * b[k * NU + u];
+        kg[q][u] = s.Kg[(k * NU + u) * 4 + i];
+        bk[q][u] = b[k * NU + u];
       }
       const int kz = k >= 1 ? 2 * k - 2 : 0;
-      if (z) acc += k >= 1 ? c0 * z[kz] + c1 * z[kz + 1] : 0.0;
-      w[q] = acc;
-      if (s.iso) {  // uniform
+      zk[q][0] = zp[kz];
+      zk[q][1] = zp[kz + 1];
+    }
+    if (s.iso) {  // uniform
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = k0 - q >= 0 ? k0 - q : 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) f[q][c] = s.SM[(k * 4 + i) * 4 + c];
-      } else {
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 - q >= 0 ? k0 - q : 0;
+      double acc = 0.0;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) acc += kg[q][u] * bk[q][u];
+      const double zt = c0 * zk[q][0] + c1 * zk[q][1];
+      acc += z && k >= 1 ? zt : 0.0;
+      w[q] = acc;
+      if (!s.iso) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           double fr = acol[c];
 #pragma unroll
-          for (int u = 0; u < NU; ++u) fr -= kgi[u] * Bm[c][u];
+          for (int u = 0; u < NU; ++u) fr -= kg[q][u] * Bm[c][u];
           f[q][c] = fr;
           *(keeper && k0 - q >= 0 ? s.SM + (k * 4 + i) * 4 + c : junk) = fr;
         }
