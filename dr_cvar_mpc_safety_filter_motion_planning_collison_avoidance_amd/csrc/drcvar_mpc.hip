@@ -203,6 +203,9 @@ enum { kSiteStart = 1, kSiteP1, kSiteP23, kSiteP4, kSitePolishHess, kSitePolishR
 constexpr int kStampProblems = 64, kStampSlots = 20;
 __device__ unsigned long long g_mpc_stamps[kStampProblems * kStampSlots];
 __device__ unsigned long long g_cl_stamps[8];  // cluster exchange sub-phases, problem 0, group 0
+// per workgroup of problem 0's cluster (index cl.id < 32), summed over its exchanges: the 100 MHz
+// clock at its arrival and at its release, and the count — relative arrival order over the cluster
+__device__ unsigned long long g_cl_arrive[3 * 32];
 // per-wave spans of the P1 phase (workgroup 0 of problem 0): [wave][0] = cycles from the barrier
 // before the factorisation to the wave's end of its P1 work, summed over iterations; [wave][1] = count
 __device__ unsigned long long g_wave_stamps[16];
@@ -1850,6 +1853,9 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
   __syncthreads();
   CL_STAMP(2);  // barrier behind the drains
   if (wave == 0) {
+#ifdef DRCVAR_MPC_STAMPS
+    const unsigned long long arr_t = __builtin_amdgcn_s_memrealtime();
+#endif
     if (lane == 0) __hip_atomic_fetch_add(cl.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long target = (static_cast<unsigned long long>(cl.epoch) + 1ull) * cl.size;
     bool gave_up = false;
@@ -1873,6 +1879,13 @@ __device__ inline void cluster_combine(Cluster& cl, const Lds& s, const double* 
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
     if (lane == 0) cx[kCxGaveUp] = gave_up ? 1.0 : 0.0;
+#ifdef DRCVAR_MPC_STAMPS
+    if (lane == 0 && blockIdx.x < static_cast<unsigned>(cl.size) && cl.id < 32) {
+      atomicAdd(&g_cl_arrive[cl.id], arr_t);
+      atomicAdd(&g_cl_arrive[32 + cl.id], __builtin_amdgcn_s_memrealtime());
+      atomicAdd(&g_cl_arrive[64 + cl.id], 1ull);
+    }
+#endif
     CL_STAMP(3);  // arrival + poll (includes waiting for the slowest workgroup)
   }
   __syncthreads();
@@ -3148,6 +3161,12 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       optimal = false;
       rollout();
     }
+#if defined(DRCVAR_MPC_STAMPS) && defined(DRCVAR_STAMP_GROUP)  // the phase stamps of another group
+    if (cid == DRCVAR_STAMP_GROUP && tid == 0 && b < kStampProblems) {
+      stamp_acc[9] = it;
+      for (int k = 0; k < kStampSlots; ++k) g_mpc_stamps[b * kStampSlots + k] = stamp_acc[k];
+    }
+#endif
     if (cid != 0) return;  // workgroup 0 writes the problem's outputs (every one holds them)
   }
   double unused = 0.0;
@@ -3170,7 +3189,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
     info[DRCVAR_MPC_INFO_POLISH_ATTEMPTS] = polish_attempts;
   }
   MPC_PHASE(8);
-#ifdef DRCVAR_MPC_STAMPS
+#if defined(DRCVAR_MPC_STAMPS) && !defined(DRCVAR_STAMP_GROUP)
   if (tid == 0 && b < kStampProblems) {
     stamp_acc[9] = it;
     for (int k = 0; k < kStampSlots; ++k) g_mpc_stamps[b * kStampSlots + k] = stamp_acc[k];
@@ -3326,6 +3345,10 @@ int drcvar_diag_cluster_stamps(unsigned long long* host) {
 int drcvar_diag_mpc_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mpc_stamps), sizeof(g_mpc_stamps), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? kStampProblems : -1;
+}
+int drcvar_diag_cluster_arrivals(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cl_arrive), sizeof(g_cl_arrive), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 96 : -1;
 }
 int drcvar_diag_wave_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_stamps), sizeof(g_wave_stamps), 0,

@@ -71,6 +71,24 @@ for shape in sys.argv[1:] or ["30,3,1", "50,256,1"]:
         names = ["partials+barrier", "combine+stores+drain", "barrier", "arrive+poll", "barrier", "gather"]
         print("  cluster exchange sub-phases (cumulative, workgroup 0):",
               ", ".join(f"{n} {cs[i] / max(cs[:6].sum(), 1) * 100:.0f}%" for i, n in enumerate(names)))
+    try:  # which workgroup of problem 0's cluster arrives last at the exchanges, and how long each waits
+        ca = lib.drcvar_diag_cluster_arrivals
+        ca.argtypes = [ctypes.c_void_p]
+        ab = (ctypes.c_ulonglong * 96)()
+        if st[16] and ca(ctypes.cast(ab, ctypes.c_void_p)) == 96:
+            a = np.frombuffer(ab, dtype=np.uint64).reshape(3, 32)
+            g = int((a[2] > 0).sum())
+            if g and len(set(a[2, :g].tolist())) == 1:
+                n = int(a[2, 0])
+                arr = a[0, :g].astype(np.float64) / n  # mean arrival clock (10 ns ticks)
+                rel = a[1, :g].astype(np.float64) / n
+                late = (arr - arr.min()) * 10.0
+                print(f"  cluster arrivals over {n} exchanges (mean ns after the earliest workgroup): " +
+                      ", ".join(f"g{i} {late[i]:.0f}" for i in range(g)))
+                print("  mean wait from arrival to release (ns): " +
+                      ", ".join(f"g{i} {(rel[i] - arr[i]) * 10.0:.0f}" for i in range(g)))
+    except AttributeError:
+        pass
     try:
         ws = lib.drcvar_diag_wave_stamps
         ws.argtypes = [ctypes.c_void_p]
