@@ -150,18 +150,37 @@ def _quoted_includes(path: str, seen=None) -> list:
     return out
 
 
+_toolchain_id = None
+
+
+def _toolchain() -> bytes:
+    """``hipcc --version`` (the compiler's identity: part of every object key and source key)."""
+    global _toolchain_id
+    if _toolchain_id is None:
+        _toolchain_id = subprocess.run(["hipcc", "--version"], capture_output=True, check=True).stdout
+    return _toolchain_id
+
+
+def _unit_flags(defs=(), extra_flags=()) -> list:
+    """The full hipcc flag list of one translation unit (what build() compiles it with)."""
+    return [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-I", INCLUDE_DIR,
+            *defs, *extra_flags]
+
+
 def source_key(basename: str = "drcvar_halfspace.hip") -> str:
     """A hash of one translation unit's inputs (its source, the headers and .inc tables it
-    includes, its extra compile flags): profiles/ evidence is tied to the kernel code it measured,
-    and bench.py uses it only while the sources still match."""
+    includes, the toolchain's identity and its full compile flags, as build() keys its object):
+    profiles/ evidence is tied to the kernel build it measured, and bench.py uses it only while
+    all of these still match."""
     import hashlib
     src = os.path.join(PKG_DIR, "csrc", basename)
     h = hashlib.sha256(open(src, "rb").read())
     for f in _quoted_includes(src):
         h.update(open(f, "rb").read())
+    h.update(_toolchain())
     for s, defs in _compile_units():
         if s == src:
-            h.update(" ".join(defs).encode())
+            h.update(" ".join(_unit_flags(defs)).replace(INCLUDE_DIR, "include").encode())
     return h.hexdigest()[:16]
 
 
@@ -179,11 +198,10 @@ def build(verbose: bool = False, extra_flags=()) -> str:
     incs = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.inc")))  # tables the sources include
     headers = b"".join(open(h, "rb").read() for h in HEADERS + incs)
     # the compiler's identity is part of every key: objects of an older hipcc / ROCm are rebuilt
-    toolchain = subprocess.run(["hipcc", "--version"], capture_output=True, check=True).stdout
+    toolchain = _toolchain()
     objs, procs = [], []
     for src, defs in _compile_units():
-        flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-I", INCLUDE_DIR,
-                 *defs, *extra_flags]
+        flags = _unit_flags(defs, extra_flags)
         key = hashlib.sha256(open(src, "rb").read() + headers + toolchain
                              + " ".join(flags).encode()).hexdigest()[:16]
         tag = "".join(d.replace("-D", ".") for d in defs if d.startswith("-D"))

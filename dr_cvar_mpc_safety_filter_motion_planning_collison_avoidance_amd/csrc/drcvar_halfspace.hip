@@ -42,13 +42,7 @@ constexpr int kMaxValueIters = 3;  // value-linear refinements before switching 
 constexpr double kSentinel = 100.0;
 // sample load forms (kernel template)
 constexpr int kLoadPair = 0, kLoadVec = 1, kLoadNt = 2;
-#ifndef DRCVAR_NT_BYTES  // diagnostic builds may move the threshold (scripts/micro A/B runs)
-#define DRCVAR_NT_BYTES (256ll << 20)
-#endif
-constexpr int64_t kNtBytes = DRCVAR_NT_BYTES;  // launches reading more than the MALL use kLoadNt
-#ifndef DRCVAR_HS_LDS_PAD  // diagnostic builds: extra dynamic LDS per workgroup (caps residency)
-#define DRCVAR_HS_LDS_PAD 0
-#endif
+constexpr int64_t kNtBytes = 256ll << 20;  // launches reading more than the MALL use kLoadNt
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 #ifdef DRCVAR_STAMPS
@@ -819,10 +813,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   double* rec = out + u * DRCVAR_OUT_WIDTH;
 
   DRCVAR_STAMP(0);
-#if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 0
-  if (tid == 0) rec[0] = 0.0;  // diagnostic build: dispatch cost only
-  return;
-#endif
 
   // ---- 1. load + moments ----------------------------------------------------------------
   // Branch-free: idle slots of the last row re-load sample n-1 and contribute zeros.  Offsets:
@@ -908,10 +898,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double mux = mom[0] * inv_n, muy = mom[1] * inv_n;
   // any non-finite sample makes a sum non-finite (so do sums that overflow): solver failure
   const bool bad = !(std::isfinite(mom[0]) && std::isfinite(mom[1]));
-#if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 1
-  if (tid == 0) rec[0] = mux + muy + (kPilot ? 0.f : mom0[0] + mom0[1] + mom0[2] + mom0[3]);
-  return;
-#endif
 
   // ---- 2. direction ----------------------------------------------------------------------
   double h0, h1;
@@ -1010,10 +996,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     }
     DRCVAR_STAMP(4);
   }
-#if defined(DRCVAR_DIAG_STAGE) && DRCVAR_DIAG_STAGE == 2
-  if (tid == 0) rec[0] = static_cast<double>(bin) + c + rr;  // diagnostic: + histogram and scan
-  return;
-#endif
 
   // ---- 4. candidates of the target bucket + tail sum below them -----------------------------
   double tau, dsum;  // dsum = sum_{d<tau} (d - tau)
@@ -1250,7 +1232,7 @@ constexpr int64_t kMaxGridY = 65535;
 template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
 int launch_form(const Launch& L) {
   const int64_t n_obs = L.units / L.n_steps;
-  const size_t dyn = DRCVAR_HS_LDS_PAD;
+  const size_t dyn = 0;
   for (int64_t o0 = 0; o0 < n_obs; o0 += kMaxGridY) {
     const int64_t chunk = n_obs - o0 < kMaxGridY ? n_obs - o0 : kMaxGridY;
     hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),

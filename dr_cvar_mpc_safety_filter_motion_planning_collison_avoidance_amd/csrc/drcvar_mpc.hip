@@ -33,6 +33,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -150,10 +151,7 @@ constexpr double kSlackHess = 100.0;  // d^2/ds^2 of 50 s^2, core/mpc_filter.py:
 constexpr double kStepFrac = 0.995;
 constexpr double kHuge = 1e300;
 constexpr int kPerStepQ = 7;          // per-step partial sums carried by one reduction
-#ifndef DRCVAR_POLISH_RHO  // diagnostic A/B builds may move it
-#define DRCVAR_POLISH_RHO 1e6
-#endif
-constexpr double kPolishRho = DRCVAR_POLISH_RHO;    // method-of-multipliers penalty of the polish
+constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the polish
 constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
@@ -739,18 +737,19 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[NU][NU], double (&inv)[N
 // Wave 0's part: the recursion (Kg, Ri into LDS; s.sc[62] = 0 on success, 1 on a failed pivot).
 // No barrier: the interior-point loop runs it beside the other waves' work (riccati_factor below
 // is the plain form: this, a barrier, riccati_factor_finish).
-#ifdef DRCVAR_NO_PIPE  // diagnostic A/B builds: the affine solve after the factorisation
-constexpr bool kPipe = false;
-#else
 constexpr bool kPipe = true;
-#endif
 // The progress words of the pipelined affine solve (int slots in s.sc[56..57]): the factorisation's
 // last finished step and the dual-residual wave's last finished input step (both count down from
 // H; kProgAbort after a failed pivot, which releases the follower).
 constexpr int kProgAbort = -1000;
 __device__ __forceinline__ int* prog_word(const Lds& s, int q) { return reinterpret_cast<int*>(s.sc + 56 + q); }
+// Release / acquire at workgroup scope, restricted to LDS (the "local" address-space fence): the
+// step's LDS stores complete before the word (one lgkmcnt wait; no global-memory wait), and the
+// reader's loads of the step's data follow its read of the word.
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
 __device__ __forceinline__ void prog_publish(const Lds& s, int q, int k) {
-  wave_lds_fence();  // the step's stores (LDS, one wave: completed in issue order) before the word
+  lds_release();
   __hip_atomic_store(prog_word(s, q), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // every lane
 }
 // (a poll is one LDS read; between polls the waiting wave sleeps ~256 cycles, a quarter of a
@@ -758,7 +757,7 @@ __device__ __forceinline__ void prog_publish(const Lds& s, int q, int k) {
 __device__ __forceinline__ void prog_wait(const Lds& s, int q, int k) {
   while (__hip_atomic_load(prog_word(s, q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > k)
     __builtin_amdgcn_s_sleep(4);
-  wave_lds_fence();
+  lds_acquire();
 }
 
 
@@ -2374,7 +2373,11 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
       if (round == 0 && a.polish && merit <= kEarlyPolishMerit && merit > kStallRatio * merit_back2) {
         converged = true;  // (the factorisation beside this P1 serves the active-set guess)
         early = true;
+        // the best iterate is this one (u, merit and iteration together): the post-loop restore
+        // and a resume after a failed early polish then start from the state the rows describe
         best_merit = merit;
+        best_it = it;
+        for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];
         break;
       }
       merit_back2 = merit_back1;
@@ -2646,7 +2649,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   if (it > it_end) it = it_end;
   __syncthreads();
   MPC_PHASE(6);
-  if (status != DRCVAR_MPC_STATUS_OPTIMAL && best_merit <= 1e3 * a.tol) {
+  if (status != DRCVAR_MPC_STATUS_OPTIMAL && !(early && round == 0) && best_merit <= 1e3 * a.tol) {
     // stalled close to the optimum (or a resumed round short of its tighter tolerance): return
     // the best iterate, its slacks re-optimised below
     status = best_merit <= a.tol ? DRCVAR_MPC_STATUS_OPTIMAL : DRCVAR_MPC_STATUS_OPTIMAL_INACCURATE;
@@ -3205,15 +3208,17 @@ __global__ void zero_counters_kernel(double* ws, int n_problems) {
 
 template <int NU, int NX, int BLK, int HMX, bool CL, bool RL>
 int launch_form(const MpcArgs& args, int64_t n_problems, size_t lds_req, size_t attr_bytes, hipStream_t stream) {
-  static bool attr_set[64] = {};  // per device; idempotent (a racing second call sets the same value)
+  // per device and kernel form, set once; the flags are atomics because any host thread may
+  // launch (a racing second caller sets the same value again, which is harmless)
+  static std::atomic<bool> attr_set[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return DRCVAR_ERR_LAUNCH;
-  if (!attr_set[dev]) {
+  if (!attr_set[dev].load(std::memory_order_acquire)) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mpc_ipm_kernel<NU, NX, BLK, HMX, CL, RL>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(attr_bytes)) != hipSuccess)
       return DRCVAR_ERR_LAUNCH;
-    attr_set[dev] = true;
+    attr_set[dev].store(true, std::memory_order_release);
   }
   // the arrival counters, zeroed in front of every launch by a one-wave kernel of agent-scope
   // (write-through) stores: a hipMemsetAsync node replayed from a hipGraph left the counters
@@ -3324,10 +3329,13 @@ int launch_nu4(const MpcArgs& args, int64_t n_problems, hipStream_t stream) { re
 int device_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  static int cached[64] = {};
-  if (dev >= 0 && dev < 64 && cached[dev] > 0) return cached[dev];
+  static std::atomic<int> cached[64] = {};  // per device (any host thread may ask)
+  if (dev >= 0 && dev < 64) {
+    const int c = cached[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (dev >= 0 && dev < 64) cached[dev] = cus;
+  if (dev >= 0 && dev < 64) cached[dev].store(cus, std::memory_order_relaxed);
   return cus;
 }
 

@@ -131,12 +131,8 @@ __global__ __launch_bounds__(kBlock) void sample_kernel(SampleArgs a) {
       const double y0 = fma(a.l10, z00, fma(a.l11, z01, ny));
       const double x1 = fma(a.l00, z10, nx);
       const double y1 = fma(a.l10, z10, fma(a.l11, z11, ny));
-#ifdef DRCVAR_SAMPLER_NO_STORE  // diagnostic: the arithmetic alone (stores only for a sentinel)
-      if (x0 + y0 + x1 + y1 == 1234.5) put_sample<kPacked, kNT>(dst + pidx * sn, x0, y0);
-#else
       put_sample<kPacked, kNT>(dst + pidx * sn, x0, y0);
       if (pidx + pairs < a.N) put_sample<kPacked, kNT>(dst + (pidx + pairs) * sn, x1, y1);
-#endif
     }
   }
 }

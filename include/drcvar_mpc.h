@@ -150,10 +150,15 @@ int32_t drcvar_mpc_launch_groups_ex(const drcvar_mpc_model* model, int64_t n_pro
  *   u_fallback [B, horizon, nu] inputs rolled out when a problem is not solved (the caller builds
  *                           them as _fallback does: shifted last optimum, else u_ref)
  *   x_out [B, horizon+1, nx], u_out [B, horizon, nu], info_out [B, DRCVAR_MPC_INFO_WIDTH]: dense
- *   workspace               drcvar_mpc_workspace_doubles() doubles; per problem it holds ten
- *                           [n_obstacles, 64] arrays h0, h1, g, s, w_hs, lambda_hs, w_s, lambda_s
- *                           (s = the slack of each halfspace at exit) and two saved across a failed
- *                           polish, then per workgroup the best iterate and the saved bound states
+ *   workspace               drcvar_mpc_workspace_doubles() doubles: scratch of the solver, whose
+ *                           contents at exit are unspecified.  Per problem it reserves ten
+ *                           [n_obstacles, 64] row arrays (h0, h1, g, s, w_hs, lambda_hs, w_s,
+ *                           lambda_s and two saved across a failed polish), then per workgroup the
+ *                           best iterate and the saved bound states.  The row arrays are used
+ *                           only by the forms that keep their rows in global memory: the clustered
+ *                           rows-in-LDS form (a cluster whose obstacle slice fits in LDS, e.g. the
+ *                           C5 hand-off) keeps its row slice in LDS and never writes them back, so
+ *                           no caller may read slacks or duals from the workspace
  *   max_iter, tol           interior-point limits (e.g. 60, 1e-7); converged when
  *                           max(|r_primal|/(1+|d|), |r_dual|/(1+|q|), mean complementarity) <= tol
  *   polish                  nonzero: finish with the active-set polish (method of multipliers on

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Copy the judged summaries of a scripts/gpu_round.sh session from gpurun_out/ (scratch) into
+# Copy the judged summaries of a scripts/gpu_run.sh session from gpurun_out/ (scratch) into
 # profiles/<round>/ (tracked):  bash scripts/collect_profiles.sh r01
 set -eu
 cd "$(dirname "$0")/.."

@@ -290,12 +290,24 @@ def _random_problem(rng, O, T, H, dyn="double", bounds=True, tight=True):
         A = np.eye(8) + 0.01 * rng.normal(size=(8, 8))
         B = 0.2 * rng.normal(size=(8, 2))
         C = np.eye(8)[:2] + 0.2 * rng.normal(size=(2, 8))
+    elif dyn == "double_full":  # the isotropic double integrator (register-form factorisation)
+        A, B, C = double_integrator()  # with a full Q, a dense output map and a coupled R
+        C = C + 0.2 * rng.normal(size=(2, 4))
+    elif dyn == "drag":  # a true 4-state, 2-input model that is not isotropic: per-axis drag
+        dt = 0.2
+        A = np.array([[1, 0, dt, 0], [0, 1, 0, dt], [0, 0, 1 - 0.3 * dt, 0], [0, 0, 0, 1 - 0.7 * dt]])
+        B = np.array([[0.5 * dt ** 2, 0], [0, 0.5 * dt ** 2], [dt, 0], [0, 1.2 * dt]])
+        C = np.eye(4)[:2]
     else:  # generic4
         A = np.eye(5) + 0.01 * rng.normal(size=(5, 5))
         B = 0.2 * rng.normal(size=(5, 4))
         C = np.eye(5)[:2]
     nx, nu = A.shape[0], B.shape[1]
     Q, R = 2 * np.eye(nx), np.eye(nu)
+    if dyn == "double_full":
+        M = rng.normal(size=(4, 4))
+        Q = M @ M.T / 4 + 0.5 * np.eye(4)
+        R = np.array([[1.0, 0.3], [0.3, 0.8]])
     x0 = np.zeros(nx)
     x0[:2] = rng.uniform(-3, 3, 2)
     x_ref = np.zeros((H + 1, nx))
@@ -405,7 +417,8 @@ def test_gpu_three_metrics_one_launch(path, dev):
     ("double", 25, 0, 0, True, True), ("single", 60, 8, 60, True, True),
     ("generic1", 64, 4, 64, True, True), ("generic3", 40, 5, 40, True, True),
     ("generic4", 30, 5, 30, True, True), ("generic44", 30, 5, 30, True, True),
-    ("generic8", 24, 4, 24, False, True),
+    ("generic8", 24, 4, 24, False, True), ("double_full", 30, 6, 30, True, True),
+    ("double_full", 50, 20, 50, True, True), ("drag", 30, 6, 30, True, True), ("drag", 50, 20, 50, True, True),
 ])
 def test_gpu_random_problems_match_oracle(dyn, H, O, T, bounds, tight, dev):
     rng = np.random.default_rng(H * 1000 + O * 10 + T)
@@ -422,6 +435,33 @@ def test_gpu_random_problems_match_oracle(dyn, H, O, T, bounds, tight, dev):
         np.testing.assert_allclose(x, xo, atol=MPC_TOL)
         assert abs(info[_native.MPC_INFO_OBJECTIVE] - io["objective"]) <= 1e-6 * max(1.0, abs(io["objective"]))
         assert abs(info[_native.MPC_INFO_MAX_SLACK] - max(io["slacks"].max(initial=0.0), 0.0)) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,O", [(30, 6), (50, 20)])
+def test_gpu_isotropic_and_general_factorisations_agree(H, O, dev):
+    """The register-form factorisation (chosen when A and B are blocks of multiples of I2, checked
+    exactly) against the general LDS form on the SAME model: A's zero (0, 1) entry set to 1e-300
+    defeats the exact check without changing the model at fp64 resolution.  A full Q, a dense C and
+    a coupled R (only A and B select the form): both forms' answers agree with each other and with
+    the oracle (the isotropic form was only ever checked with Q = 2I, C = [I 0])."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    rng = np.random.default_rng(7 * H + O)
+    for trial in range(3):
+        pr = _random_problem(rng, O, H, H, "double_full")
+        iso = mf.MPCModel(pr["A"], pr["B"], pr["C"], pr["Q"], pr["R"], H, pr["ub"], pr["pb"], device=dev)
+        A2 = pr["A"].copy()
+        A2[0, 1] = 1e-300
+        gen = mf.MPCModel(A2, pr["B"], pr["C"], pr["Q"], pr["R"], H, pr["ub"], pr["pb"], device=dev)
+        assert iso.host_blob[-1] == 1.0 and gen.host_blob[-1] == 0.0   # the ISO flag of each
+        _, uo, io = _oracle(pr)
+        x1, u1, i1 = _gpu(pr, dev)
+        x2, u2, i2 = _gpu(dict(pr, A=A2), dev)
+        for u, info in ((u1, i1), (u2, i2)):
+            assert int(info[_native.MPC_INFO_STATUS]) == _native.MPC_STATUS_OPTIMAL, info
+            np.testing.assert_allclose(u, uo, atol=MPC_TOL, err_msg=f"H={H} O={O} trial {trial}")
+        np.testing.assert_allclose(u1, u2, atol=1e-9)
+        np.testing.assert_allclose(x1, x2, atol=1e-9)
 
 
 @pytest.mark.gpu
@@ -625,3 +665,34 @@ def test_gpu_h30_straggler_matches_oracle(dev):
         assert (info[:, _native.MPC_INFO_ITERATIONS] <= float(z["kernel_iterations"])).all(), info[0]
         np.testing.assert_allclose(u.cpu().numpy(), np.repeat(z["u_expected"][None], Bn, 0), atol=MPC_TOL)
         assert np.all(np.abs(info[:, _native.MPC_INFO_OBJECTIVE] - float(z["objective"])) <= 1e-9 * float(z["objective"]))
+
+
+@pytest.mark.gpu
+def test_gpu_failed_early_polish_resumes_to_the_oracle(dev):
+    """The straggler leaves its first round by the early polish (a stall at merit <= 1e-3);
+    options.debug_force_resume makes that polish give up at once, so the solve resumes the
+    interior-point method from the early iterate (its u, slacks and duals together) to the normal
+    tolerance and polishes there: the answer must still be the oracle's, alone and in a 160-problem
+    batch (the many-problem form) (the early break once left an older u beside the
+    current rows)."""
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
+    z, _ = _h30_straggler()
+    A, B, C = double_integrator()
+    H = z["x_ref"].shape[0] - 1
+    model = mf.MPCModel(A, B, C, 2 * np.eye(4), np.eye(2), H, tuple(z["u_bounds"]), tuple(z["p_bounds"]),
+                        device=dev)
+    Tt = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)
+    base = mf.filter_batch(model, Tt(z["h"][None]), Tt(z["g"][None]), Tt(z["x0"][None]), Tt(z["x_ref"][None]),
+                           Tt(np.zeros((1, H, 2))))[2][0].cpu().numpy()
+    for Bn in (1, 160):
+        rep = lambda a: Tt(np.repeat(a[None], Bn, axis=0))
+        x, u, info = mf.filter_batch(model, rep(z["h"]), rep(z["g"]), rep(z["x0"]), rep(z["x_ref"]),
+                                     Tt(np.zeros((Bn, H, 2))), options=mf.make_options(debug_force_resume=True))
+        info = info.cpu().numpy()
+        assert (info[:, _native.MPC_INFO_STATUS] == _native.MPC_STATUS_OPTIMAL).all(), info[0]
+        assert (info[:, _native.MPC_INFO_POLISHED] == 1).all(), info[0]
+        # the resumed round really ran: more interior-point iterations than the early exit took
+        assert (info[:, _native.MPC_INFO_ITERATIONS] > base[_native.MPC_INFO_ITERATIONS]).all(), (info[0], base)
+        np.testing.assert_allclose(u.cpu().numpy(), np.repeat(z["u_expected"][None], Bn, 0), atol=MPC_TOL)
+        np.testing.assert_allclose(x.cpu().numpy(), np.repeat(z["x_expected"][None], Bn, 0), atol=MPC_TOL)
