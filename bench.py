@@ -50,6 +50,10 @@ sys.path.insert(0, REPO)
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import engine, sharding, synthetic  # noqa: E402
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.engine import RiskParams  # noqa: E402
 
+# chunk counts of the pipelined RCCL step per strong-scaling workload (--chunks auto): C4's
+# all-gather is latency-bound (~123 KB), two chunks at most; C5's shard kernel is long enough
+# (~40 us at 8 ranks) to hide a chunk's gather behind the next chunk's kernel
+CHUNKS = {"c2": [2], "c3": [2], "c4": [2], "c5": [2, 4]}
 WORKLOADS = {
     # name: (obstacles, steps, samples, description)
     "c2": (4, 20, 1000, "multi_obstacle-like synthetic, 4 obstacles, T=20, N=1000 (BASELINE config 2)"),
@@ -186,13 +190,20 @@ def cpu_baseline(samples, ego, params, budget_s):
 
 class Stepper:
     """Issues exactly the requested number of steps of a `ShardedBatch` — the kernel (`compute`)
-    and/or the RCCL all-gather (`exchange`, world > 1) — as eager ctypes launches, or as hipGraph
-    replays: a graph of G = min(graph_batch, steps) steps replayed steps // G times plus a graph
-    of the remainder (and one of the warm-up count), so the steps issued are the steps asked for.
-    If capturing fails (e.g. a collective the backend cannot capture) the stepper falls back to
-    eager launches in the same process and says so in describe()."""
+    and/or the exchange (`exchange`, world > 1: the RCCL all-gather or the peer-push
+    publish/wait) — as eager ctypes launches, or as hipGraph replays: a graph of G =
+    min(graph_batch, steps) steps replayed steps // G times plus a graph of the remainder (and one
+    of the warm-up count), so the steps issued are the steps asked for.
 
-    def __init__(self, sb, mode, graph_batch, steps, dev, exchange=True, compute=True, warmup=0):
+    The ranks AGREE on graph vs eager before any graph runs: every rank captures its graphs
+    (capturing executes nothing), then a MIN all-reduce of the success flags over the control
+    group (gloo, so it cannot be caught in a half-enqueued RCCL capture) decides, and only then
+    are the graphs uploaded by one replay each.  If any rank's capture failed, every rank drops
+    its graphs and launches eagerly — never one rank replaying a captured collective while another
+    issues it eagerly, which would pair collectives of different steps or hang."""
+
+    def __init__(self, sb, mode, graph_batch, steps, dev, exchange=True, compute=True, warmup=0,
+                 world=1, ctrl=None):
         self.sb, self.mode, self.dev = sb, mode, dev
         self.exchange = exchange and sb.full is not None
         self.compute = compute
@@ -201,21 +212,30 @@ class Stepper:
         if mode == "graph":
             self._one()                       # warm the code objects (and the communicator)
             torch.cuda.synchronize(dev)
+            why = None
             try:
                 for n in sorted({self.G, steps % self.G, warmup % self.G} - {0}):
                     self.graphs[n] = self._capture(n)
             except Exception as exc:          # noqa: BLE001 - reported, then eager launches
-                self.mode, self.G, self.graphs = "eager", 1, {}
-                self.fallback = f"hipGraph capture failed ({type(exc).__name__}: {exc}); eager launches"
+                why = f"{type(exc).__name__}: {exc}"
+                torch.cuda.synchronize(dev)
+            ok = agree(world, ctrl, why is None)
+            if not ok:
+                self.mode, self.G, self.graphs, self._keep = "eager", 1, {}, []
+                self.fallback = (f"hipGraph capture failed ({why}); eager launches" if why else
+                                 "hipGraph capture failed on another rank; eager launches on every rank")
+            else:
+                for n in sorted(self.graphs):
+                    self.graphs[n].replay()   # upload the executable graphs outside any timed region
                 torch.cuda.synchronize(dev)
 
     def _one(self, launch=None):
         if self.compute and self.exchange:
-            self.sb.step(launch)          # kernel + all-gather (pipelined by chunks when chunks > 1)
+            self.sb.step(launch)          # kernel + exchange (RCCL: pipelined by chunks when chunks > 1)
         elif self.compute:
             self.sb.compute(launch)
         elif self.exchange:
-            self.sb.exchange()
+            self.sb.exchange(launch)
 
     def _capture(self, n):
         g = torch.cuda.CUDAGraph()
@@ -224,7 +244,6 @@ class Stepper:
             for _ in range(n):
                 self._one(launch)
         self._keep.append(launch)
-        g.replay()                            # upload the executable graph outside any timed region
         return g
 
     def run(self, steps):
@@ -255,6 +274,15 @@ class Stepper:
             return (f"hipGraph replays of {self.G} steps" + (f" (+ graphs of {extra})" if extra else "")
                     + f"; step = {what}")
         return f"eager; step = {what}"
+
+
+def agree(world, ctrl, ok):
+    """True on every rank iff `ok` on every rank (a MIN all-reduce over the gloo control group)."""
+    if world == 1:
+        return bool(ok)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
+    return bool(flag.item())
 
 
 def timed(world, fn, dev, stream):
@@ -298,8 +326,12 @@ def main():
     ap.add_argument("--strong-workloads", default="c4,c5",
                     help="global batches of the strong-scaling legs (sharded over the ranks), comma-separated")
     ap.add_argument("--strong-steps", type=int, default=20)
-    ap.add_argument("--chunks", type=int, default=2,
-                    help="strong-scaling legs at N > 1: also time the pipelined step with this many chunks")
+    ap.add_argument("--chunks", default="auto",
+                    help="strong-scaling legs at N > 1: also time the RCCL step pipelined in these chunk "
+                         "counts (comma-separated; auto = per workload, CHUNKS)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "peer"],
+                    help="strong-scaling legs at N > 1: auto = time the RCCL all-gather and the peer-push "
+                         "exchange and report the faster as the leg's step; rccl / peer = that one only")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -327,9 +359,11 @@ def main():
         raise SystemExit(f"LOCAL_RANK {local_rank} but only {ndev} GPUs visible")
     dev = torch.device("cuda", local_rank % ndev)
     torch.cuda.set_device(dev)
+    ctrl = None   # the control group: host-side agreement / handle exchange, never on a GPU stream
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            ctrl = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
     gdev = "cpu" if (world > 1 and args.dist_backend == "gloo") else None
@@ -343,14 +377,15 @@ def main():
     ego = synthetic.straight_line_ego(T, dev)
     sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=42, gather_device=gdev)
     assert sb.count == O * T
-    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev, exchange=False, warmup=args.warmup)
+    stepper = Stepper(sb, mode, args.graph_batch, args.steps, dev, exchange=False, warmup=args.warmup,
+                      world=world, ctrl=ctrl)
     stepper.run(args.warmup)                   # untimed warmup (W steps, the same launch path)
     elapsed, ev_s, K = timed(world, lambda: stepper.run(args.steps), dev, stream)
     kernel_s, ktiming = ev_s / K, "HIP events over the timed region / K (launch gaps included)"
 
     strong = None
     if not args.no_large and not args.no_strong:
-        strong = {w: strong_scaling(args, world, rank, dev, stream, params, gdev, mode, w)
+        strong = {w: strong_scaling(args, world, rank, dev, stream, params, gdev, mode, w, ctrl)
                   for w in args.strong_workloads.split(",") if w}
 
     result = None
@@ -421,68 +456,121 @@ def main():
     return result
 
 
-def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload):
+def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload, ctrl=None):
     """The north-star multi-GPU form (BASELINE configs 4 and 5): ONE global batch sharded over
-    the ranks — each rank draws only its contiguous unit block on its device, the kernel writes
-    into its slice of the all-gather input and the records are all-gathered over RCCL inside the
-    timed region.  Identical global work at every N (strong scaling); at N = 1 the exchange is
-    the identity and is skipped.  Besides the whole step, each phase is timed alone and reported
-    as its maximum over the ranks: `kernel_ms` (the shard's launch) and `allgather_ms` (the
-    collective alone, the same records).  For C5 also the full MPC loop (shard kernel ->
-    all-gather -> the DR-CVaR QP over all O*T halfspaces, replicated per rank)."""
+    the ranks — each rank draws only its contiguous unit block on its device and the records are
+    reassembled on every rank inside the timed region.  Identical global work at every N (strong
+    scaling); at N = 1 the exchange is the identity and is skipped.
+
+    At N > 1 every exchange form is timed on the same draw (`exchanges`): the RCCL
+    all_gather_into_tensor of the records, the same pipelined behind the kernel in the chunk
+    counts of CHUNKS[workload], and the peer-push exchange (sharding.PeerExchange: the kernel
+    writes every record into every rank's region over xGMI; one launch publishes, waits and
+    copies), each checked to give records bitwise equal to the plain RCCL step's.  The leg's
+    `value` / `ms_per_step` are the fastest equal form's (named in `exchange`).  Each phase is
+    also timed alone, as its maximum over the ranks: `kernel_ms` (the shard's launch),
+    `allgather_ms` (the RCCL collective alone) and `peer_exchange_ms` (the publish/wait/copy
+    launch alone).  For C5 also the full MPC loop (shard kernel -> exchange -> the DR-CVaR QP
+    over all O*T halfspaces, replicated per rank) and main.py's three filters."""
     O, T, N, desc = WORKLOADS[workload]
     seed = 7 if workload == "c5" else 11
     nominal = synthetic.nominal_paths(O, T, dev, seed=seed)
     ego = synthetic.straight_line_ego(T, dev)
     sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed, gather_device=gdev)
     K = args.strong_steps
-    st = Stepper(sb, mode, 10, K, dev)
-    st.run(min(K, 10))
-    elapsed, _, _ = timed(world, lambda: st.run(K), dev, stream)
-    launch = st.describe()
-    del st
+
+    def run_form(sbx):
+        st = Stepper(sbx, mode, 10, K, dev, world=world, ctrl=ctrl)
+        st.run(min(K, 10))
+        el, _, _ = timed(world, lambda: st.run(K), dev, stream)
+        return el, st.describe()
+
+    elapsed, launch = run_form(sb)
     # phases alone, rank-max (HIP events on the launching stream, K steps each)
-    kst = Stepper(sb, mode, 10, K, dev, exchange=False)
+    kst = Stepper(sb, mode, 10, K, dev, exchange=False, world=world, ctrl=ctrl)
     kst.run(min(K, 10))
     _, kernel_s, _ = timed(world, lambda: kst.run(K), dev, stream)
     del kst
     gather_ms = None
     if world > 1:
-        gst = Stepper(sb, mode, 10, K, dev, compute=False)
+        gst = Stepper(sb, mode, 10, K, dev, compute=False, world=world, ctrl=ctrl)
         gst.run(min(K, 10))
         _, gather_s, _ = timed(world, lambda: gst.run(K), dev, stream)
         gather_ms = gather_s / K * 1e3
         del gst
     kernel_s /= K
+    exchanges = {"rccl": {"ms_per_step": elapsed / K * 1e3, "launch": launch,
+                          "what": "all_gather_into_tensor of the 64-B records after the kernel"}}
+    best, best_el, best_sb = "rccl", elapsed, sb
+    peer_ms = None
+    if world > 1:
+        ref = sb.records()
+        chunk_list = CHUNKS[workload] if args.chunks == "auto" else [int(c) for c in args.chunks.split(",") if c]
+        if args.exchange in ("auto", "rccl"):
+            for c in chunk_list:
+                if c < 2:
+                    continue
+                # the pipelined step (sharding.chunked_all_gather): the rank's block in `chunks`
+                # launches, chunk j's all-gather issued behind chunk j + 1's kernel
+                sbc = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed,
+                                            gather_device=gdev, chunks=c)
+                el_c, launch_c = run_form(sbc)
+                same = agree(world, ctrl, bool(torch.equal(sbc.records().to(ref.device), ref)))
+                step_c = el_c / K * 1e3
+                exchanges[f"rccl_chunks{c}"] = {
+                    "chunks": c, "ms_per_step": step_c, "records_equal_rccl": same, "launch": launch_c,
+                    "overlap_ms": kernel_s * 1e3 + gather_ms - step_c}
+                if same and el_c < best_el:
+                    best, best_el, best_sb = f"rccl_chunks{c}", el_c, sbc
+                else:
+                    del sbc
+        if args.exchange in ("auto", "peer"):   # (gloo rehearsal too: ranks sharing one GPU map each other)
+            try:
+                sbp = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed,
+                                            exchange="peer", ctrl=ctrl, samples=sb.samples)
+            except sharding.PeerExchangeUnavailable as exc:
+                exchanges["peer"] = {"unavailable": str(exc)}
+            else:
+                el_p, launch_p = run_form(sbp)
+                err = sbp.peer.error()
+                same = err == 0 and bool(torch.equal(sbp.records().to(ref.device), ref))
+                same = agree(world, ctrl, same)
+                pst = Stepper(sbp, mode, 10, K, dev, compute=False, world=world, ctrl=ctrl)
+                pst.run(min(K, 10))
+                _, peer_s, _ = timed(world, lambda: pst.run(K), dev, stream)
+                del pst
+                peer_ms = peer_s / K * 1e3
+                exchanges["peer"] = {
+                    "ms_per_step": el_p / K * 1e3, "records_equal_rccl": same, "error_word": err,
+                    "launch": launch_p, "exchange_alone_ms": peer_ms,
+                    "what": "the kernel writes every record into every rank's region (IPC-mapped, "
+                            "xGMI); one launch publishes the step, waits for every peer's and copies"}
+                if same and el_p < best_el:
+                    best, best_el, best_sb = "peer", el_p, sbp
+                else:
+                    sbp.close()
+                    del sbp
     out = {"workload": f"{workload}: {desc}, global batch sharded over {world} rank(s)",
-           "value": sb.U * K / elapsed, "unit": "halfspace-constraints/s", "n_gpus": world,
-           "steps": K, "ms_per_step": elapsed / K * 1e3, "scaling": "strong",
+           "value": sb.U * K / best_el, "unit": "halfspace-constraints/s", "n_gpus": world,
+           "steps": K, "ms_per_step": best_el / K * 1e3, "scaling": "strong",
+           "exchange": best if world > 1 else None,
            "units_global": sb.U, "units_per_rank": sb.per,
            "bytes_per_rank": sb.algorithmic_bytes,
            "record_bytes_gathered": sb.per * world * 64 if world > 1 else 0,
-           "parallelism": f"dp{world}" + (f"+allgather ({'RCCL' if gdev is None else 'gloo'})"
+           "parallelism": f"dp{world}" + (f"+{best} ({'RCCL' if gdev is None else 'gloo'} control)"
                                            if world > 1 else ""),
-           "launch": launch,
+           "launch": exchanges[best]["launch"],
            "phases_rank_max": {"kernel_ms": kernel_s * 1e3, "allgather_ms": gather_ms,
+                               "peer_exchange_ms": peer_ms,
                                "timing": f"HIP events over {K} steps of the phase alone, max over ranks"},
            "kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK,
            # one rank: HBM bytes per launch of the whole batch from the committed PMC passes
            # (profiles/pmc_traffic.json), against bytes_per_rank (the algorithmic bytes)
            "traffic": load_traffic(workload) if world == 1 else None}
-    if world > 1 and args.chunks > 1:
-        # the pipelined step (sharding.chunked_all_gather): the rank's block in `chunks` launches,
-        # chunk j's all-gather issued behind chunk j + 1's kernel; same records, same order
-        sbc = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed, gather_device=gdev,
-                                    chunks=args.chunks)
-        stc = Stepper(sbc, mode, 10, K, dev)
-        stc.run(min(K, 10))
-        el_c, _, _ = timed(world, lambda: stc.run(K), dev, stream)
-        same = bool(torch.equal(sbc.records().to(sb.records().device), sb.records()))
-        step_c = el_c / K * 1e3
-        out["pipelined"] = {"chunks": args.chunks, "value": sb.U * K / el_c, "ms_per_step": step_c,
-                            "overlap_ms": kernel_s * 1e3 + gather_ms - step_c,
-                            "records_equal_unpipelined": same, "launch": stc.describe()}
-        del stc, sbc
+    if world > 1:
+        out["exchanges"] = exchanges
+    if best_sb is not sb:
+        sb = best_sb          # the loops below run on the leg's fastest exchange
     # full loop: + the QP hand-off on every rank (core/mpc_filter.py:116-151 takes all halfspaces)
     if workload == "c5" and not args.no_mpc:
         import numpy as np
@@ -570,6 +658,7 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload)
         large["halfspaces_per_s"] = sb.U / kernel_s
         large["timing"] = f"HIP events over {K} graph-replayed launches (replays of 10)"
         out["_roofline"] = large
+    sb.close()   # collective for the peer exchange (every rank chose the same form); else a no-op
     return out
 
 

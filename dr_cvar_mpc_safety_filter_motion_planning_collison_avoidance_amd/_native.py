@@ -1,5 +1,6 @@
 """Loader for the HIP engine (``_lib/libdrcvar_halfspace.so``) — the C ABI of
-``include/drcvar_halfspace.h`` bound with ctypes.
+``include/drcvar_halfspace.h`` (+ ``drcvar_mpc.h``, ``drcvar_sampling.h``, ``drcvar_exchange.h``)
+bound with ctypes.
 
 There is deliberately no fallback: if the shared library is missing or cannot be loaded every
 entry point raises :class:`NativeLibraryError`.  ``build()`` compiles it for gfx950 in-tree.
@@ -17,13 +18,14 @@ LIB_DIR = os.path.join(PKG_DIR, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libdrcvar_halfspace.so")
 SOURCES = [os.path.join(PKG_DIR, "csrc", "drcvar_halfspace.hip"),
            os.path.join(PKG_DIR, "csrc", "drcvar_mpc.hip"),
-           os.path.join(PKG_DIR, "csrc", "drcvar_sampling.hip")]
+           os.path.join(PKG_DIR, "csrc", "drcvar_sampling.hip"),
+           os.path.join(PKG_DIR, "csrc", "drcvar_exchange.hip")]
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("drcvar_halfspace.h", "drcvar_mpc.h",
-                                                  "drcvar_sampling.h")]
+                                                  "drcvar_sampling.h", "drcvar_exchange.h")]
 OFFLOAD_ARCH = "gfx950"  # CDNA4 only
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OUT_WIDTH = 8
 MAX_SAMPLES = 16384               # largest unit held on chip (register plans)
 MAX_SAMPLES_STREAM = 2 ** 31 - 1  # larger units run the streaming kernel
@@ -64,6 +66,18 @@ class MpcOptions(ctypes.Structure):
                 ("reserved", ctypes.c_int32 * 2)]
 
 
+# peer-push exchange (include/drcvar_exchange.h)
+MAX_PEERS = 8
+PEER_HANDLE_BYTES = 64
+
+
+class PeerSet(ctypes.Structure):
+    """``drcvar_peer_set`` (include/drcvar_exchange.h)."""
+
+    _fields_ = [("region", ctypes.c_void_p * MAX_PEERS), ("rows", ctypes.c_int64),
+                ("state", ctypes.c_void_p), ("n_ranks", ctypes.c_int32), ("rank", ctypes.c_int32)]
+
+
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "drcvar_abi_version",
@@ -82,6 +96,14 @@ EXPORTED_SYMBOLS = (
     "drcvar_mpc_filter_f64_ex",
     "drcvar_sample_trajectories_f64",
     "drcvar_sample_units_f64",
+    "drcvar_peer_region_doubles",
+    "drcvar_peer_alloc",
+    "drcvar_peer_free",
+    "drcvar_peer_open",
+    "drcvar_peer_close",
+    "drcvar_peer_can_access",
+    "drcvar_peer_signal_wait",
+    "drcvar_safe_halfspaces_f64_peer",
 )
 
 
@@ -280,6 +302,24 @@ def _bind(lib):
     lib.drcvar_sample_units_f64.argtypes = [
         ptr, i64, i64, i64, i64, i64, i64, i64, dbl, dbl, dbl, u64, u64, i32, ptr, i64, i64, ptr]
     lib.drcvar_sample_units_f64.restype = ctypes.c_int
+    peerp = ctypes.POINTER(PeerSet)
+    lib.drcvar_peer_region_doubles.argtypes = [i64]
+    lib.drcvar_peer_region_doubles.restype = i64
+    lib.drcvar_peer_alloc.argtypes = [i64, ctypes.POINTER(ctypes.c_void_p), ptr]
+    lib.drcvar_peer_alloc.restype = ctypes.c_int
+    lib.drcvar_peer_free.argtypes = [ptr]
+    lib.drcvar_peer_free.restype = ctypes.c_int
+    lib.drcvar_peer_open.argtypes = [ptr, ctypes.POINTER(ctypes.c_void_p)]
+    lib.drcvar_peer_open.restype = ctypes.c_int
+    lib.drcvar_peer_close.argtypes = [ptr]
+    lib.drcvar_peer_close.restype = ctypes.c_int
+    lib.drcvar_peer_can_access.argtypes = [i32, i32, i32p]
+    lib.drcvar_peer_can_access.restype = ctypes.c_int
+    lib.drcvar_peer_signal_wait.argtypes = [peerp, ptr, i64, ptr]
+    lib.drcvar_peer_signal_wait.restype = ctypes.c_int
+    lib.drcvar_safe_halfspaces_f64_peer.argtypes = [
+        ptr, i64, i64, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, peerp, i64, ptr, ptr]
+    lib.drcvar_safe_halfspaces_f64_peer.restype = ctypes.c_int
     return lib
 
 

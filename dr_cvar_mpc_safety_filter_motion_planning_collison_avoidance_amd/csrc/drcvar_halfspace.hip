@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstdint>
 
+#include "drcvar_exchange.h"
 #include "drcvar_halfspace.h"
 
 namespace {
@@ -486,6 +487,44 @@ __device__ __forceinline__ void store_record(double* rec, double m0, double m1, 
   reinterpret_cast<double2*>(rec)[3] = make_double2(gs, gt);
 }
 
+// The peer-push exchange (drcvar_safe_halfspaces_f64_peer, include/drcvar_exchange.h): every
+// rank's launch writes each record straight into the exchange region of every rank of the node
+// (its own and, over xGMI, the peers' — regions mapped into this process by IPC), at the record's
+// global row, in the buffer of this step's parity; drcvar_peer_signal_wait then publishes and
+// awaits the generation.  The regions are uncached device memory, and the stores are system-scope
+// (write-through) so that no L2 holds a record a peer's later read could miss.
+struct PeerArgs {
+  double* region[DRCVAR_MAX_PEERS];    // rank j's region (parity 0 rows, parity 1 rows, flags)
+  int64_t rows;                        // records per parity buffer (n_ranks * per)
+  int64_t row_base;                    // global row of this launch's unit 0
+  const unsigned long long* gen;       // this rank's completed-step counter (device)
+  int32_t n_ranks;
+};
+
+__device__ __forceinline__ void store_sys(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One record to every rank's region: lane j < n_ranks writes rank j's copy (values uniform across
+// the wave).  Parity = (completed steps + 1) & 1: the buffer this step fills.
+__device__ __forceinline__ void peer_store_record(const PeerArgs& pa, unsigned long long gen,
+                                                  int64_t u, int lane, double m0, double m1,
+                                                  double gm, double h0, double h1, double gc,
+                                                  double gs, double gt) {
+  if (lane < pa.n_ranks) {
+    const int64_t parity = static_cast<int64_t>((gen + 1ull) & 1ull);
+    double* r = pa.region[lane] + (parity * pa.rows + pa.row_base + u) * DRCVAR_OUT_WIDTH;
+    store_sys(r + 0, m0);
+    store_sys(r + 1, m1);
+    store_sys(r + 2, gm);
+    store_sys(r + 3, h0);
+    store_sys(r + 4, h1);
+    store_sys(r + 5, gc);
+    store_sys(r + 6, gs);
+    store_sys(r + 7, gt);
+  }
+}
+
 // d_i = h . xi_i — one expression, used both for the register-resident samples and for re-reads,
 // so both paths see bitwise-identical values (core/risk_metrics.py:145,233: h @ samples.T)
 __device__ __forceinline__ double project(double h0, double h1, double x, double y) {
@@ -740,6 +779,8 @@ __device__ __forceinline__ int32_t failure_status(bool nonfinite, const Params& 
 }
 
 // Offsets from the lower-tail statistics (wave 0, lane 0 writes).  L = tau + dsum / k.
+// (The peer form below computes the same values in every lane of wave 0, from lane 0's tau and
+// dsum, and writes the whole record — the mean halfspace too — to every rank.)
 // r = R_c |h| (risk_metrics.py:293, :234), computed by the caller as soon as h is known.
 template <int NW>
 __device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, double r, double h0,
@@ -765,6 +806,24 @@ __device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, d
   }
 }
 
+__device__ __forceinline__ void finish_offsets_peer(const PeerArgs& pa, unsigned long long gen,
+                                                    int64_t u, const Params& prm, double r,
+                                                    double h0, double h1, double tau, double dsum,
+                                                    double mux, double muy, int lane) {
+  tau = readlane_f64(tau, 0);
+  dsum = readlane_f64(dsum, 0);
+  const double L = tau + dsum * prm.inv_k;
+  const double g_cvar = r - prm.delta - L;
+  double g_star = kSentinel, g_tilde = kSentinel - r;
+  if (prm.epsilon >= 0.0) {
+    g_star = r - prm.delta + prm.eps_over_alpha - L;
+    g_tilde = g_star - r;
+  }
+  double m0, m1, g_mean;
+  mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
+  peer_store_record(pa, gen, u, lane, m0, m1, g_mean, h0, h1, g_cvar, g_star, g_tilde);
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // the fused kernel
@@ -776,12 +835,15 @@ __device__ __forceinline__ void finish_offsets(double* rec, const Params& prm, d
 //            256 MB Infinity Cache, whose samples are streamed exactly once)
 //   GIVEN_H  `dir` holds h per unit (cvar_halfspace / dr_cvar_halfspace) instead of ego per step
 // ---------------------------------------------------------------------------------------------
-template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
+//   PEER     the peer-push exchange form: records go to every rank's exchange region (PeerArgs)
+//            instead of `out`
+template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H, bool PEER>
 __global__ void __launch_bounds__(BLOCK)
 safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n,
                       int64_t s_obs, int64_t s_step, int64_t s_samp,
                       const double* __restrict__ dir, int64_t dir_s_obs, int64_t dir_s_step,
-                      Params prm, double* __restrict__ out, int32_t* __restrict__ status) {
+                      Params prm, double* __restrict__ out, int32_t* __restrict__ status,
+                      PeerArgs peer) {
   constexpr int NW = BLOCK / kWave;
   constexpr int NB = 1 << LOG_NB;
   __shared__ uint32_t hist[hist_words<NB>()];
@@ -860,6 +922,8 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   const double inv_k = prm.inv_k;
   asm volatile("" ::"s"(e0), "s"(e1), "s"(px), "s"(py), "s"(inv_n), "s"(inv_n0), "s"(deg_sq),
                "s"(z_lo), "s"(hist_scale), "s"(inv_k), "s"(status));
+  unsigned long long gen = 0;  // the peer form's completed-step counter (parity of the buffer)
+  if constexpr (PEER) gen = *peer.gen;
   // the histogram is cleared while the sample loads are in flight (barrier 1 orders it before
   // the first atomic)
 #pragma unroll
@@ -908,6 +972,17 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     separating_direction(mux, muy, e0, e1, deg_sq, &h0, &h1);
   }
   if (bad || prm.unbounded) {  // solver failure, risk_metrics.py:298-303,334-338
+    if constexpr (PEER) {
+      if (wave == 0) {
+        const double r = prm.rc * norm_h(h0, h1);  // R_c |h|
+        double m0, m1, g_mean;
+        mean_halfspace(mux, muy, prm.rc, &m0, &m1, &g_mean);
+        peer_store_record(peer, gen, u, lane, m0, m1, g_mean, h0, h1, kSentinel, kSentinel,
+                          kSentinel - r);
+        if (status && lane == 0) status[u] = failure_status(bad, prm);
+      }
+      return;
+    }
     if (tid == 0) {
       const double r = prm.rc * norm_h(h0, h1);  // R_c |h|
       double m0, m1, g_mean;
@@ -1027,7 +1102,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     __syncthreads();                                                      // [barrier 3]
     DRCVAR_STAMP(6);
     if (wave != 0) {
-      if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
+      if (!PEER && wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
     }
     // the per-wave candidate counts are read in the same batch as the tail partials (the ranking
@@ -1082,14 +1157,17 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
                                         &tau, &dsum);
     }
     if (wave != 0) {
-      if (wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
+      if (!PEER && wave == 1) write_mean_halfspace(rec, mux, muy, prm.rc, lane);
       return;
     }
     rch = prm.rc * norm_h(h0, h1);
   }
 
   // ---- 5. offsets (wave 0) -------------------------------------------------------------------
-  finish_offsets<NW>(rec, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
+  if constexpr (PEER)
+    finish_offsets_peer(peer, gen, u, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
+  else
+    finish_offsets<NW>(rec, prm, rch, h0, h1, tau, dsum, mux, muy, lane);
   if (status && lane == 0) status[u] = failure_status(false, prm);
   DRCVAR_STAMP(7);
 }
@@ -1223,30 +1301,33 @@ struct Launch {
   double* out;
   int32_t* status;  // [units] or null
   hipStream_t stream;
+  PeerArgs peer;    // the peer form only
 };
 
 // grid (n_steps, obstacles), at most kMaxGridY obstacles per launch (the y-dimension limit):
 // larger batches are split into obstacle chunks on the host
 constexpr int64_t kMaxGridY = 65535;
 
-template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H>
+template <int BLOCK, int P, int LOG_NB, int LOAD, bool GIVEN_H, bool PEER>
 int launch_form(const Launch& L) {
   const int64_t n_obs = L.units / L.n_steps;
   const size_t dyn = 0;
   for (int64_t o0 = 0; o0 < n_obs; o0 += kMaxGridY) {
     const int64_t chunk = n_obs - o0 < kMaxGridY ? n_obs - o0 : kMaxGridY;
-    hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H>),
+    PeerArgs pa = L.peer;
+    pa.row_base += o0 * L.n_steps;
+    hipLaunchKernelGGL((safe_halfspace_kernel<BLOCK, P, LOG_NB, LOAD, GIVEN_H, PEER>),
                        dim3(static_cast<unsigned>(L.n_steps), static_cast<unsigned>(chunk)),
                        dim3(BLOCK), dyn, L.stream, L.samples + o0 * L.s_obs, L.n_steps,
                        static_cast<int>(L.n), L.s_obs, L.s_step, L.s_samp,
                        L.dir + o0 * L.dir_s_obs, L.dir_s_obs, L.dir_s_step, L.prm,
                        L.out + o0 * L.n_steps * DRCVAR_OUT_WIDTH,
-                       L.status ? L.status + o0 * L.n_steps : nullptr);
+                       L.status ? L.status + o0 * L.n_steps : nullptr, pa);
   }
   return DRCVAR_OK;
 }
 
-template <int BLOCK, int P, int LOG_NB, bool GIVEN_H>
+template <int BLOCK, int P, int LOG_NB, bool GIVEN_H, bool PEER>
 int launch_plan(Launch L, bool vec) {
   const int64_t sub = P <= 8 ? kWave : BLOCK;  // the window's subsample: pilot or row 0 (kernel)
   L.prm.inv_n0 = 1.0 / static_cast<double>(L.n < sub ? L.n : sub);
@@ -1254,9 +1335,10 @@ int launch_plan(Launch L, bool vec) {
   // measured on C5 (2.05 GB): nontemporal 16-B loads 0.746 of HBM peak vs 0.715; on C3 (3.2 MB,
   // cache-resident across steps) they cost 3 %, so only launches larger than the MALL use them
   const bool nt = vec && L.units * L.n * 16 > kNtBytes;
-  if (nt) return launch_form<BLOCK, P, LOG_NB, kLoadNt, GIVEN_H>(L);
-  if (vec) return launch_form<BLOCK, P, LOG_NB, kLoadVec, GIVEN_H>(L);
-  return launch_form<BLOCK, P, LOG_NB, kLoadPair, GIVEN_H>(L);
+  if (nt) return launch_form<BLOCK, P, LOG_NB, kLoadNt, GIVEN_H, PEER>(L);
+  if (vec) return launch_form<BLOCK, P, LOG_NB, kLoadVec, GIVEN_H, PEER>(L);
+  if constexpr (PEER) return DRCVAR_ERR_UNSUPPORTED;  // the peer form reads packed 16-B samples
+  else return launch_form<BLOCK, P, LOG_NB, kLoadPair, GIVEN_H, false>(L);
 }
 
 template <bool GIVEN_H>
@@ -1273,13 +1355,13 @@ void launch_stream(const Launch& L, bool vec) {
   }
 }
 
-template <bool GIVEN_H>
+template <bool GIVEN_H, bool PEER = false>
 int dispatch(const Launch& L, int threads, int per) {
   if (L.units == 0) return DRCVAR_OK;
   const bool vec = (reinterpret_cast<uintptr_t>(L.samples) % 16 == 0) && (L.s_obs % 2 == 0) &&
                    (L.s_step % 2 == 0) && (L.s_samp % 2 == 0);
   if (L.n > DRCVAR_MAX_SAMPLES) {  // beyond the register plans: the streaming kernel
-    if (threads != 0 || per != 0) return DRCVAR_ERR_UNSUPPORTED;
+    if (PEER || threads != 0 || per != 0) return DRCVAR_ERR_UNSUPPORTED;
     if (L.n > DRCVAR_MAX_SAMPLES_STREAM) return DRCVAR_ERR_UNSUPPORTED;
     (void)hipGetLastError();
     launch_stream<GIVEN_H>(L, vec);
@@ -1290,20 +1372,27 @@ int dispatch(const Launch& L, int threads, int per) {
   (void)hipGetLastError();  // clear stale errors from unrelated work
   int rc = DRCVAR_OK;
   switch (p) {
-    case 0: rc = launch_plan<64, 2, 7, GIVEN_H>(L, vec); break;
-    case 1: rc = launch_plan<128, 4, 8, GIVEN_H>(L, vec); break;
-    case 2: rc = launch_plan<256, 4, 9, GIVEN_H>(L, vec); break;
-    case 3: rc = launch_plan<256, 8, 10, GIVEN_H>(L, vec); break;
-    case 4: rc = launch_plan<256, 16, 10, GIVEN_H>(L, vec); break;
-    case 5: rc = launch_plan<256, 20, 10, GIVEN_H>(L, vec); break;
-    case 6: rc = launch_plan<512, 16, 10, GIVEN_H>(L, vec); break;
-    case 7: rc = launch_plan<512, 20, 10, GIVEN_H>(L, vec); break;
-    case 8: rc = launch_plan<1024, 12, 10, GIVEN_H>(L, vec); break;
-    case 9: rc = launch_plan<1024, 16, 10, GIVEN_H>(L, vec); break;
-    case 10: rc = launch_plan<64, 16, 9, GIVEN_H>(L, vec); break;
-    case 11: rc = launch_plan<128, 8, 9, GIVEN_H>(L, vec); break;
-    case 12: rc = launch_plan<512, 2, 9, GIVEN_H>(L, vec); break;
-    default: rc = launch_plan<1024, 10, 10, GIVEN_H>(L, vec); break;
+    case 0: rc = launch_plan<64, 2, 7, GIVEN_H, PEER>(L, vec); break;
+    case 1: rc = launch_plan<128, 4, 8, GIVEN_H, PEER>(L, vec); break;
+    case 2: rc = launch_plan<256, 4, 9, GIVEN_H, PEER>(L, vec); break;
+    case 3: rc = launch_plan<256, 8, 10, GIVEN_H, PEER>(L, vec); break;
+    case 4: rc = launch_plan<256, 16, 10, GIVEN_H, PEER>(L, vec); break;
+    case 5: rc = launch_plan<256, 20, 10, GIVEN_H, PEER>(L, vec); break;
+    case 6: rc = launch_plan<512, 16, 10, GIVEN_H, PEER>(L, vec); break;
+    case 7: rc = launch_plan<512, 20, 10, GIVEN_H, PEER>(L, vec); break;
+    case 8: rc = launch_plan<1024, 12, 10, GIVEN_H, PEER>(L, vec); break;
+    case 9: rc = launch_plan<1024, 16, 10, GIVEN_H, PEER>(L, vec); break;
+    default:
+      if constexpr (PEER) {
+        return DRCVAR_ERR_UNSUPPORTED;  // tuning geometries: not in the peer form
+      } else {
+        switch (p) {
+          case 10: rc = launch_plan<64, 16, 9, GIVEN_H, false>(L, vec); break;
+          case 11: rc = launch_plan<128, 8, 9, GIVEN_H, false>(L, vec); break;
+          case 12: rc = launch_plan<512, 2, 9, GIVEN_H, false>(L, vec); break;
+          default: rc = launch_plan<1024, 10, 10, GIVEN_H, false>(L, vec); break;
+        }
+      }
   }
   if (rc != DRCVAR_OK) return rc;
   return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
@@ -1371,17 +1460,32 @@ int safe_halfspaces(const double* samples, int64_t n_obstacles, int64_t n_steps,
                     int64_t stride_sample, const double* ego_ref_pos, int64_t ego_stride_step,
                     double robot_radius, double obstacle_radius, double alpha, double delta,
                     double epsilon, double* out, int32_t* status, void* stream, int threads,
-                    int per) {
+                    int per, const drcvar_peer_set* peers = nullptr, int64_t row_base = 0) {
   if (n_obstacles < 0 || n_steps < 0 || n_samples < 1) return DRCVAR_ERR_INVALID_ARGUMENT;
   if (!params_ok(robot_radius, obstacle_radius, alpha, delta, epsilon))
     return DRCVAR_ERR_INVALID_ARGUMENT;
   const int64_t units = n_obstacles * n_steps;
   if (units == 0) return DRCVAR_OK;
-  if (!samples || !ego_ref_pos || !out || units > 0x7fffffff) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (!samples || !ego_ref_pos || (!out && !peers) || units > 0x7fffffff)
+    return DRCVAR_ERR_INVALID_ARGUMENT;
   Launch L{samples, units, n_steps, n_samples, stride_obstacle, stride_step, stride_sample,
            ego_ref_pos, 0, ego_stride_step,
            make_params(robot_radius, obstacle_radius, alpha, delta, epsilon, n_samples), out,
            status, static_cast<hipStream_t>(stream)};
+  if (peers) {
+    const drcvar_peer_set& ps = *peers;
+    if (ps.n_ranks < 1 || ps.n_ranks > DRCVAR_MAX_PEERS || ps.rank < 0 || ps.rank >= ps.n_ranks ||
+        !ps.state || ps.rows < 0 || row_base < 0 || row_base + units > ps.rows)
+      return DRCVAR_ERR_INVALID_ARGUMENT;
+    for (int j = 0; j < ps.n_ranks; ++j)
+      if (!ps.region[j]) return DRCVAR_ERR_INVALID_ARGUMENT;
+    for (int j = 0; j < DRCVAR_MAX_PEERS; ++j) L.peer.region[j] = j < ps.n_ranks ? ps.region[j] : nullptr;
+    L.peer.rows = ps.rows;
+    L.peer.row_base = row_base;
+    L.peer.gen = ps.state;
+    L.peer.n_ranks = ps.n_ranks;
+    return dispatch<false, true>(L, 0, 0);
+  }
   return dispatch<false>(L, threads, per);
 }
 
@@ -1465,6 +1569,20 @@ int drcvar_safe_halfspaces_f64_v2(const double* samples, int64_t n_obstacles, in
                          stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
                          obstacle_radius, alpha, delta, epsilon, out, status, stream,
                          threads_per_unit, samples_per_thread);
+}
+
+int drcvar_safe_halfspaces_f64_peer(const double* samples, int64_t n_obstacles, int64_t n_steps,
+                                    int64_t n_samples, int64_t stride_obstacle, int64_t stride_step,
+                                    int64_t stride_sample, const double* ego_ref_pos,
+                                    int64_t ego_stride_step, double robot_radius,
+                                    double obstacle_radius, double alpha, double delta,
+                                    double epsilon, const drcvar_peer_set* peers, int64_t row_base,
+                                    int32_t* status, void* stream) {
+  if (!peers) return DRCVAR_ERR_INVALID_ARGUMENT;
+  return safe_halfspaces(samples, n_obstacles, n_steps, n_samples, stride_obstacle, stride_step,
+                         stride_sample, ego_ref_pos, ego_stride_step, robot_radius,
+                         obstacle_radius, alpha, delta, epsilon, nullptr, status, stream, 0, 0,
+                         peers, row_base);
 }
 
 int drcvar_offsets_given_h_f64_v2(const double* samples, int64_t n_units, int64_t n_samples,

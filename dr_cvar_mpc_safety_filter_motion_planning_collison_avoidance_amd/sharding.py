@@ -21,17 +21,177 @@ Two forms:
   :meth:`ShardedBatch.step` is one launch + one ``all_gather_into_tensor``.  This is the
   north-star multi-GPU form ``bench.py`` times.
 
-``compute`` is injectable in :func:`sharded_safe_halfspaces` so the partition/gather logic can be
-exercised with world_size 2 on CPU (gloo) in the tests; the product path always passes the HIP
-engine.
+Two exchanges for :class:`ShardedBatch`:
+
+* ``"rccl"`` — the portable one: ``all_gather_into_tensor`` of the records (RCCL over xGMI with
+  the ``nccl`` backend), optionally pipelined behind the kernel by chunks
+  (:func:`chunked_all_gather`);
+* ``"peer"`` — the MI355X-native one (:class:`PeerExchange`, ``include/drcvar_exchange.h``): each
+  rank's halfspace launch writes every record straight into every rank's exchange region (mapped
+  by IPC, written over xGMI), and one small launch per step publishes and awaits the step's
+  generation and copies the gathered records out — the exchange rides inside the kernel and only
+  a flag round trip is left after it.  Set up only when every rank can map every peer's memory;
+  all ranks agree (over the control group) before any rank uses it, otherwise every rank keeps
+  ``"rccl"``.
+
+``compute`` is injectable in :func:`sharded_safe_halfspaces`, and the sampler / launch preparation
+in :class:`ShardedBatch`, so the partition/gather logic can be exercised with world_size 2 and 4
+on CPU (gloo) in the tests; the product path always uses the HIP engine.
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 import torch.distributed as dist
 
-from . import engine
+from . import _native, engine
 from .engine import RiskParams
+
+
+class PeerExchangeUnavailable(RuntimeError):
+    """Some rank cannot map or access some peer's exchange region (every rank raises it)."""
+
+
+class PeerExchange:
+    """The peer-push record exchange of one rank (``include/drcvar_exchange.h``).
+
+    ``rows`` records per parity buffer (the padded global batch, ``world * per``).  Collective:
+    every rank of ``group`` constructs it together.  The region handles and device indices go
+    round the control group (``ctrl``: a gloo group; the default group when it is gloo itself);
+    each rank maps every peer's region, checks that its device can access every peer's device,
+    and all ranks agree on the outcome before any of them uses it — if anything fails on any rank,
+    every rank raises :class:`PeerExchangeUnavailable` (and has released what it mapped).
+    ``out`` (``[rows, 8]``, an ordinary device tensor) holds the gathered records after
+    :meth:`signal_wait`.  ``spin_limit_us`` bounds every wait for a peer (then ``error()`` is
+    non-zero instead of a hang)."""
+
+    def __init__(self, rows: int, world: int, rank: int, device: torch.device, ctrl=None,
+                 spin_limit_us: int = 2_000_000):
+        if not (1 <= world <= _native.MAX_PEERS):
+            raise PeerExchangeUnavailable(f"peer exchange supports 1..{_native.MAX_PEERS} ranks, not {world}")
+        lib = _native.lib()
+        self.rows, self.world, self.rank, self.device = int(rows), world, rank, device
+        self.spin_limit_us = int(spin_limit_us)
+        self._lib = lib
+        self._ctrl = ctrl
+        self._own = ctypes.c_void_p()
+        self._opened = []
+        handle = (ctypes.c_char * _native.PEER_HANDLE_BYTES)()
+        doubles = lib.drcvar_peer_region_doubles(self.rows)
+        with torch.cuda.device(device):
+            rc = lib.drcvar_peer_alloc(doubles, ctypes.byref(self._own), handle)
+        ok = rc == _native.OK
+        why = None if ok else f"rank {rank}: drcvar_peer_alloc -> {rc}"
+        mine = (bytes(handle), device.index if ok else -1)
+        infos = [None] * world
+        if world > 1:
+            dist.all_gather_object(infos, mine, group=ctrl)
+        else:
+            infos = [mine]
+        regions = [None] * world
+        if ok:
+            regions[rank] = self._own.value
+            for j, (h, d) in enumerate(infos):
+                if j == rank:
+                    continue
+                can = ctypes.c_int32(0)
+                if d < 0 or lib.drcvar_peer_can_access(device.index, d, ctypes.byref(can)) != _native.OK \
+                        or not can.value:
+                    ok, why = False, f"rank {rank}: device {device.index} cannot access rank {j}'s device {d}"
+                    break
+                r = ctypes.c_void_p()
+                with torch.cuda.device(device):
+                    rc = lib.drcvar_peer_open((ctypes.c_char * _native.PEER_HANDLE_BYTES).from_buffer_copy(h),
+                                              ctypes.byref(r))
+                if rc != _native.OK:
+                    ok, why = False, f"rank {rank}: drcvar_peer_open(rank {j}) -> {rc}"
+                    break
+                self._opened.append(r.value)
+                regions[j] = r.value
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
+            reasons = [None] * world
+            dist.all_gather_object(reasons, why, group=ctrl)
+            why = "; ".join(r for r in reasons if r) or why
+        if not int(flag.item()):
+            self._release()   # nothing was ever written through a mapping: no barrier needed
+            raise PeerExchangeUnavailable(why or "a peer rank could not set up the exchange")
+        self.state = torch.zeros(3, dtype=torch.int64, device=device)   # generation, counter, error
+        self.out = torch.empty((self.rows, engine.OUT_WIDTH), dtype=torch.float64, device=device)
+        ps = _native.PeerSet()
+        for j in range(world):
+            ps.region[j] = regions[j]
+        ps.rows, ps.state, ps.n_ranks, ps.rank = self.rows, self.state.data_ptr(), world, rank
+        self.peers = ps
+        self._ps_ref = ctypes.byref(ps)
+        self._out_ptr = ctypes.c_void_p(self.out.data_ptr())
+        self._spin = ctypes.c_int64(self.spin_limit_us)
+
+    def signal_wait(self, stream=None) -> None:
+        """Publish this rank's step, wait for every peer's, copy the gathered records to ``out``
+        (one launch on ``stream``, default the current stream)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        code = self._lib.drcvar_peer_signal_wait(self._ps_ref, self._out_ptr, self._spin,
+                                                  ctypes.c_void_p(int(s.cuda_stream)))
+        if code != _native.OK:
+            _native.check(code)
+
+    def prepare_launch(self, samples: torch.Tensor, ego: torch.Tensor, params: RiskParams, row_base: int,
+                       stream=None) -> engine.PreparedLaunch:
+        """Freeze one ``drcvar_safe_halfspaces_f64_peer`` call over an ``[O, T, N, 2]`` block whose
+        unit 0 is global row ``row_base``."""
+        params.validate()
+        engine._check_samples(samples, 4)
+        O, T, N, _ = samples.shape
+        engine._check_pairs(ego, "ego", T, samples.device)
+        if row_base < 0 or row_base + O * T > self.rows:
+            raise ValueError(f"rows [{row_base}, {row_base + O * T}) outside the exchange's {self.rows}")
+        args = (ctypes.c_void_p(samples.data_ptr()), O, T, N, samples.stride(0), samples.stride(1),
+                samples.stride(2), ctypes.c_void_p(ego.data_ptr()), ego.stride(0),
+                params.robot_radius, params.obstacle_radius, params.alpha, params.delta, params.epsilon,
+                self._ps_ref, int(row_base), ctypes.c_void_p(None),
+                ctypes.c_void_p(engine._stream_handle(samples.device, stream)))
+        return engine.PreparedLaunch(self._lib.drcvar_safe_halfspaces_f64_peer, args, (samples, ego, self))
+
+    def generation(self) -> int:
+        return int(self.state[0].item())
+
+    def error(self) -> int:
+        """0, or bit 63 | bit j for every rank j whose flag a wait gave up on."""
+        return int(self.state[2].item()) & 0xFFFFFFFFFFFFFFFF
+
+    def close(self) -> None:
+        """Collective: wait until this device and (a barrier on the control group) every peer
+        have finished writing, then unmap the peers' regions and free the own one — a region
+        freed while a slower peer still writes into it would fault that peer."""
+        if not (self._opened or self._own.value):
+            return
+        torch.cuda.synchronize(self.device)
+        if self.world > 1:
+            dist.barrier(group=self._ctrl)
+        self._release()
+
+    def _release(self) -> None:
+        for r in self._opened:
+            self._lib.drcvar_peer_close(ctypes.c_void_p(r))
+        self._opened = []
+        if self._own.value:
+            self._lib.drcvar_peer_free(self._own)
+            self._own = ctypes.c_void_p()
+
+    def __del__(self):
+        # one rank: nothing else writes the region, so it can go with the object; several: the
+        # region stays mapped until close() or process exit (freeing it here, at a rank-local
+        # moment, could fault a peer still writing into it)
+        try:
+            if self.world == 1:
+                if self._own.value:
+                    torch.cuda.synchronize(self.device)
+                self._release()
+        except Exception:  # noqa: BLE001 - interpreter teardown
+            pass
 
 
 def block_units(n_units: int, world_size: int, align: int = 1) -> int:
@@ -171,6 +331,14 @@ def sharded_safe_halfspaces(samples: torch.Tensor, ego: torch.Tensor, params: Ri
     return full[:O * T].reshape(O, T, engine.OUT_WIDTH)
 
 
+class _Prepared(list):
+    """The frozen launches of a rank's block (one per chunk) and the stream they are bound to."""
+
+    def __init__(self, launches, stream):
+        super().__init__(launches)
+        self.stream = stream
+
+
 class ShardedBatch:
     """One rank's block of a global ``[O, T, N, 2]`` obstacle-sample batch that no rank holds.
 
@@ -178,16 +346,34 @@ class ShardedBatch:
     rank).  The rank's units ``[start, stop)`` are drawn once on its device
     (``drcvar_sample_units_f64``: sample for sample what the whole batch would hold), laid out flat
     ``[count, N, 2]`` and evaluated as ONE launch of a ``[1, count]`` grid whose per-unit ego is
-    ``ego[u mod T]``.  The kernel writes into ``send[:count]``, the all-gather input itself; with
+    ``ego[u mod T]``.
+
+    ``exchange="rccl"``: the kernel writes into ``send[:count]``, the all-gather input itself; with
     ``world > 1`` :meth:`step` then runs ``all_gather_into_tensor(full, send)`` — on RCCL the
-    records go device to device, nothing is staged.  ``records()`` is the global ``[O, T, 8]``.
+    records go device to device, nothing is staged (``chunks > 1``: pipelined behind the kernel).
+    ``exchange="peer"``: a :class:`PeerExchange` (collective set-up over ``ctrl``; raises
+    :class:`PeerExchangeUnavailable` on every rank when any rank cannot use it) — the kernel writes
+    every record into every rank's region and :meth:`step` adds the one publish/wait/copy launch;
+    ``full`` is the exchange's output.  ``records()`` is the global ``[O, T, 8]`` either way.
+
+    ``sample_fn(nominal, n, start, count, cov, seed=, stream_offset=, zero_first_step=)`` and
+    ``prepare_fn(samples [1, c, N, 2], ego [c, 2], params, out [1, c, 8], stream)`` are test-only
+    injections (CPU rehearsal of the partition and exchange logic over gloo); the product path
+    uses the device sampler and the HIP engine.  ``samples`` reuses another form's draw of the
+    same block.
     """
 
     def __init__(self, nominal: torch.Tensor, ego: torch.Tensor, n_samples: int, params: RiskParams,
                  world_size: int = 1, rank: int = 0, group=None, seed: int = 42,
                  stream_offset: int = 0, noise_cov=None, zero_first_step: bool = True,
-                 gather_device=None, chunks: int = 1, force_exchange: bool = False):
+                 gather_device=None, chunks: int = 1, force_exchange: bool = False,
+                 exchange: str = "rccl", ctrl=None, sample_fn=None, prepare_fn=None,
+                 samples: torch.Tensor | None = None):
         from .simulation import obstacles
+        if exchange not in ("rccl", "peer"):
+            raise ValueError(f"exchange must be 'rccl' or 'peer', not {exchange!r}")
+        if exchange == "peer" and (chunks != 1 or gather_device is not None):
+            raise ValueError("the peer exchange runs inside the kernel: one chunk, device records")
         O, T = int(nominal.shape[0]), int(nominal.shape[1])
         dev = nominal.device
         self.O, self.T, self.N = O, T, int(n_samples)
@@ -200,23 +386,36 @@ class ShardedBatch:
         self.per = block_units(self.U, world_size, self.chunks)
         self.cs = self.per // self.chunks if self.per else 0
         cov = obstacles.NOISE_COV if noise_cov is None else noise_cov
-        self.samples = obstacles.sample_units_device(nominal, self.N, self.start, self.count, cov,
-                                                     seed=seed, stream_offset=stream_offset,
-                                                     zero_first_step=zero_first_step)
+        if samples is not None:   # another form of the same block (bench.py: one draw, several exchanges)
+            if tuple(samples.shape) != (self.count, self.N, 2):
+                raise ValueError(f"samples must be this block's [{self.count}, {self.N}, 2]")
+            self.samples = samples
+        else:
+            sample = sample_fn if sample_fn is not None else obstacles.sample_units_device
+            self.samples = sample(nominal, self.N, self.start, self.count, cov, seed=seed,
+                                  stream_offset=stream_offset, zero_first_step=zero_first_step)
+        self._prepare_fn = prepare_fn if prepare_fn is not None else engine.prepare_safe_halfspaces
         idx = torch.arange(self.start, self.stop, device=dev) % T
         self.ego_units = ego.index_select(0, idx).contiguous()            # [count, 2], built once
         self.send = torch.zeros((self.per, engine.OUT_WIDTH), dtype=torch.float64, device=dev)
         gdev = dev if gather_device is None else torch.device(gather_device)
-        # force_exchange: the collective runs at world 1 too (tests / the 1-rank RCCL rehearsal)
-        exchange = world_size > 1 or force_exchange
-        self.full = (torch.empty((self.per * world_size, engine.OUT_WIDTH), dtype=torch.float64,
-                                 device=gdev) if exchange else None)
-        self.scratch = (torch.empty((self.chunks, world_size * self.cs, engine.OUT_WIDTH),
-                                    dtype=torch.float64, device=gdev)
-                        if exchange and self.chunks > 1 else None)
+        # force_exchange: the collective runs at world 1 too (tests / the 1-rank rehearsals)
+        do_exchange = world_size > 1 or force_exchange
+        self.exchange_kind = exchange if do_exchange else None
+        self.peer = None
+        self.scratch = None
+        if do_exchange and exchange == "peer":
+            self.peer = PeerExchange(self.per * world_size, world_size, rank, dev, ctrl=ctrl)
+            self.full = self.peer.out
+        else:
+            self.full = (torch.empty((self.per * world_size, engine.OUT_WIDTH), dtype=torch.float64,
+                                     device=gdev) if do_exchange else None)
+            self.scratch = (torch.empty((self.chunks, world_size * self.cs, engine.OUT_WIDTH),
+                                        dtype=torch.float64, device=gdev)
+                            if do_exchange and self.chunks > 1 else None)
         self._launch = self.prepare()
 
-    def prepare(self, stream=None):
+    def prepare(self, stream=None) -> _Prepared:
         """Frozen launches of this rank's block on ``stream`` (default: the current stream), one
         per chunk — for hipGraph capture pass the capturing stream."""
         launches = []
@@ -225,45 +424,66 @@ class ShardedBatch:
             if a == b:
                 launches.append(None)
                 continue
-            launch, _ = engine.prepare_safe_halfspaces(
-                self.samples[a:b].unsqueeze(0), self.ego_units[a:b], self.params,
-                out=self.send[a:b].view(1, b - a, engine.OUT_WIDTH), stream=stream)
+            if self.peer is not None:
+                launch = self.peer.prepare_launch(self.samples[a:b].unsqueeze(0), self.ego_units[a:b],
+                                                  self.params, self.start + a, stream=stream)
+            else:
+                launch, _ = self._prepare_fn(
+                    self.samples[a:b].unsqueeze(0), self.ego_units[a:b], self.params,
+                    out=self.send[a:b].view(1, b - a, engine.OUT_WIDTH), stream=stream)
             launches.append(launch)
-        return launches
+        return _Prepared(launches, stream)
 
     def _compute_chunk(self, launches, j) -> None:
         if launches[j] is not None:
             launches[j]()
 
     def compute(self, launch=None) -> None:
-        """The halfspace kernel over this rank's units (no collective)."""
+        """The halfspace kernel over this rank's units (no collective; the peer form's kernel
+        writes the records into every rank's region, but publishes nothing)."""
         launches = launch if launch is not None else self._launch
         for j in range(self.chunks):
             self._compute_chunk(launches, j)
 
-    def exchange(self) -> None:
-        """The QP hand-off exchange: every rank's records to every rank (no-op at world 1)."""
-        if self.full is not None:
+    def exchange(self, launch=None) -> None:
+        """The QP hand-off exchange: every rank's records to every rank (no-op without one)."""
+        if self.peer is not None:
+            launches = launch if launch is not None else self._launch
+            self.peer.signal_wait(launches.stream)
+        elif self.full is not None:
             chunked_all_gather(self.full, self.send, self.chunks, None, self.scratch, self.group)
 
     def step(self, launch=None) -> None:
-        """One step: the kernel and the exchange — with ``chunks > 1`` pipelined, chunk j's
-        all-gather behind chunk j + 1's kernel (:func:`chunked_all_gather`)."""
+        """One step: the kernel and the exchange — RCCL with ``chunks > 1`` pipelined (chunk j's
+        all-gather behind chunk j + 1's kernel, :func:`chunked_all_gather`); peer: the kernel
+        (records already pushed to every rank) and the publish/wait/copy launch."""
         launches = launch if launch is not None else self._launch
         if self.full is None:
             self.compute(launches)
+            return
+        if self.peer is not None:
+            self.compute(launches)
+            self.peer.signal_wait(launches.stream)
             return
         chunked_all_gather(self.full, self.send, self.chunks,
                            lambda j: self._compute_chunk(launches, j), self.scratch, self.group)
 
     def local_records(self) -> torch.Tensor:
-        """``[count, 8]`` records of this rank's units (a view of the all-gather input)."""
+        """``[count, 8]`` records of this rank's units (the peer form: after a step, from the
+        gathered output)."""
+        if self.peer is not None:
+            return self.full[self.start:self.stop]
         return self.send[:self.count]
 
     def records(self) -> torch.Tensor:
         """Global ``[O, T, 8]`` records (after :meth:`step`; at world 1 the local block)."""
         src = self.full if self.full is not None else self.send
         return src[:self.U].view(self.O, self.T, engine.OUT_WIDTH)
+
+    def close(self) -> None:
+        """Collective for the peer exchange (see :meth:`PeerExchange.close`); no-op otherwise."""
+        if self.peer is not None:
+            self.peer.close()
 
     @property
     def algorithmic_bytes(self) -> int:

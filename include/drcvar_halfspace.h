@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define DRCVAR_ABI_VERSION 2 /* 2: MPC options / cluster statuses, per-unit status outputs */
+#define DRCVAR_ABI_VERSION 3 /* 2: MPC options / cluster statuses, per-unit status outputs;
+                                3: the peer-push exchange (drcvar_exchange.h) */
 
 /* return codes */
 #define DRCVAR_OK 0

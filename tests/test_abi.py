@@ -11,7 +11,7 @@ from conftest import REPO
 from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
 
 HEADERS = [os.path.join(REPO, "include", h) for h in ("drcvar_halfspace.h", "drcvar_mpc.h",
-                                                     "drcvar_sampling.h")]
+                                                     "drcvar_sampling.h", "drcvar_exchange.h")]
 
 
 def _declared_functions():
@@ -43,7 +43,7 @@ def test_library_holds_gfx950_code_object():
 
 def test_abi_version_and_strerror():
     lib = _native.lib()
-    assert lib.drcvar_abi_version() == _native.ABI_VERSION == 2
+    assert lib.drcvar_abi_version() == _native.ABI_VERSION == 3
     assert lib.drcvar_strerror(0) == b"ok"
     assert lib.drcvar_strerror(1) == b"invalid argument"
     assert lib.drcvar_strerror(99) == b"unknown error"
@@ -99,3 +99,36 @@ def test_host_side_argument_validation():
                                           None, None) == _native.OK
     assert lib.drcvar_offsets_given_h_f64(None, 3, 0, 10, 2, None, 2, 0.3, 0.3, 0.2, 0.1, 0.15,
                                           None, None) == _native.ERR_INVALID_ARGUMENT
+
+
+def test_peer_exchange_host_side():
+    """include/drcvar_exchange.h: the region size, the peer-set struct and the host-side checks of
+    the exchange entries (none of these calls reaches a device)."""
+    lib = _native.lib()
+    assert ctypes.sizeof(_native.PeerSet) == 8 * 8 + 8 + 8 + 4 + 4
+    assert lib.drcvar_peer_region_doubles(100) == 2 * 100 * 8 + 64
+    assert lib.drcvar_peer_region_doubles(-1) == -1
+    can = ctypes.c_int32(0)
+    assert lib.drcvar_peer_can_access(0, 0, ctypes.byref(can)) == _native.OK and can.value == 1
+    assert lib.drcvar_peer_can_access(-1, 0, ctypes.byref(can)) == _native.ERR_INVALID_ARGUMENT
+    ps = _native.PeerSet()
+    ps.n_ranks, ps.rank, ps.rows, ps.state = 2, 0, 10, 16
+    ps.region[0] = 16
+    out = ctypes.c_void_p(16)
+    assert lib.drcvar_peer_signal_wait(ctypes.byref(ps), out, 1000, None) == _native.ERR_INVALID_ARGUMENT  # region[1]
+    ps.region[1] = 16
+    assert lib.drcvar_peer_signal_wait(ctypes.byref(ps), None, 1000, None) == _native.ERR_INVALID_ARGUMENT
+    assert lib.drcvar_peer_signal_wait(ctypes.byref(ps), out, 0, None) == _native.ERR_INVALID_ARGUMENT
+    ps.rank = 2
+    assert lib.drcvar_peer_signal_wait(ctypes.byref(ps), out, 1000, None) == _native.ERR_INVALID_ARGUMENT
+    ps.rank = 0
+    peer = lambda **kw: lib.drcvar_safe_halfspaces_f64_peer(
+        ctypes.c_void_p(16), kw.get("O", 1), kw.get("T", 4), kw.get("N", 10), 80, 20, 2, ctypes.c_void_p(16),
+        2, 0.3, 0.3, 0.2, 0.1, 0.15, kw.get("ps", ctypes.byref(ps)), kw.get("base", 0), None, None)
+    assert peer(ps=None) == _native.ERR_INVALID_ARGUMENT
+    assert peer(base=7) == _native.ERR_INVALID_ARGUMENT              # rows 7..10 > 10 rows
+    assert peer(base=-1) == _native.ERR_INVALID_ARGUMENT
+    assert peer(N=_native.MAX_SAMPLES + 1) == _native.ERR_UNSUPPORTED  # register plans only
+    assert peer(O=0) == _native.OK                                     # empty: nothing launched
+    assert lib.drcvar_peer_alloc(0, ctypes.byref(ctypes.c_void_p()), out) == _native.ERR_INVALID_ARGUMENT
+    assert lib.drcvar_peer_open(None, ctypes.byref(ctypes.c_void_p())) == _native.ERR_INVALID_ARGUMENT

@@ -83,3 +83,84 @@ def test_block_alignment():
     assert sharding.block_units(1920, 8, 1) == 240 and sharding.block_units(1920, 8, 3) == 240
     assert sharding.block_units(15, 2, 4) == 8 and sharding.shard_bounds(15, 2, 1, align=4) == (8, 15)
     assert sharding.shard_bounds(3, 2, 1, align=4) == (3, 3)
+
+
+# ---- ShardedBatch (the form bench.py times) at world sizes 2 and 4, chunked and not -------------
+
+def _global_batch(O, T, N):
+    rng = np.random.default_rng(7)
+    nominal = torch.from_numpy(rng.normal(size=(O, T, 2)) * 5)
+    samples = nominal[:, :, None, :] + torch.from_numpy(rng.normal(size=(O, T, N, 2)))
+    ego = torch.from_numpy(rng.normal(size=(T, 2)))
+    return nominal, samples, ego
+
+
+def _sharded_worker(rank, world, port, O, T, N, chunk_list, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        nominal, whole, ego = _global_batch(O, T, N)
+        flat = whole.reshape(O * T, N, 2)
+
+        def sample_fn(nom, n, start, count, cov, seed=0, stream_offset=0, zero_first_step=True):
+            return flat[start:start + count].clone()          # this rank's units only
+
+        def prepare_fn(samples, ego_u, p, out=None, stream=None):
+            return (lambda: _oracle_compute(samples, ego_u, p, out)), out
+
+        got = {}
+        for chunks in chunk_list:
+            sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), world, rank, chunks=chunks,
+                                       sample_fn=sample_fn, prepare_fn=prepare_fn)
+            for _ in range(2):                                 # repeated steps reuse the buffers
+                sb.step()
+            got[chunks] = (sb.records().clone().numpy(), sb.start, sb.stop, sb.local_records().numpy().copy())
+        # graph-vs-eager agreement (bench.Stepper): one rank's failure makes every rank eager
+        votes = (bench.agree(world, None, True), bench.agree(world, None, rank != world - 1))
+        q.put((rank, got, votes))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,O,T,N,chunk_list", [
+    (2, 3, 5, 40, [1, 2]), (4, 3, 5, 40, [1, 2, 4]),
+    (4, 1, 5, 17, [1, 2, 3]),      # U = 5 over 4 ranks: the tail rank(s) hold zero units
+    (4, 6, 7, 30, [1, 2]), (2, 1, 1, 9, [1, 2]),
+])
+def test_sharded_batch_steps_match_single_process(world, O, T, N, chunk_list):
+    """bench.py's strong-scaling step (sharding.ShardedBatch: per-rank draw, the kernel into the
+    all-gather input, the exchange — pipelined by chunks or not) at world sizes 2 and 4 over gloo,
+    with the C oracle as the shard compute: every rank ends with exactly the single-process
+    records, every chunking gives the same bytes, blocks tile [0, U), and a rank with no units
+    takes part in every collective; the graph-vs-eager vote is unanimous."""
+    from oracle import c_oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, O, T, N, chunk_list, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nominal, whole, ego = _global_batch(O, T, N)
+    ref = c_oracle.safe_halfspaces(whole.numpy(), ego.numpy(), 0.3, 0.3, 0.2, 0.1, 0.15)
+    empty_ranks = 0
+    for rank, got, votes in results:
+        assert votes == (True, False), (rank, votes)
+        for chunks in chunk_list:
+            rec, a, b, local = got[chunks]
+            np.testing.assert_array_equal(rec, ref)
+            np.testing.assert_array_equal(local, ref.reshape(O * T, 8)[a:b])
+            empty_ranks += (a == b) and chunks == chunk_list[0]
+    for chunks in chunk_list:
+        spans = sorted((got[chunks][1], got[chunks][2]) for _, got, _ in results)
+        assert spans[0][0] == 0 and spans[-1][1] == O * T
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    if O * T < world * 2:
+        assert empty_ranks >= 1

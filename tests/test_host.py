@@ -138,12 +138,12 @@ def test_product_loader_reads_no_environment():
 
 def test_profile_evidence_key_covers_the_unit_and_its_includes():
     """bench.py's roofline uses committed kernel-time evidence only while _native.source_key()
-    matches: the key hashes the halfspace unit, the headers it includes and its flags -- not the
-    MPC or sampler headers, whose edits do not change the halfspace kernel."""
+    matches: the key hashes the halfspace unit, the headers it includes, the toolchain and its
+    flags -- not the MPC or sampler headers, whose edits do not change the halfspace kernel."""
     import os
     from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import _native
     src = os.path.join(_native.PKG_DIR, "csrc", "drcvar_halfspace.hip")
     incs = [os.path.basename(f) for f in _native._quoted_includes(src)]
-    assert incs == ["drcvar_halfspace.h"]
+    assert incs == ["drcvar_exchange.h", "drcvar_halfspace.h"]
     assert _native.source_key() == _native.source_key("drcvar_halfspace.hip")
     assert _native.source_key("drcvar_mpc.hip") != _native.source_key()
