@@ -5,15 +5,20 @@
 // already wrote its records into every rank's region; what is left per step is one small launch:
 //
 //   publish   workgroup 0, lane j < n_ranks: flag[rank] of rank j's region <- g (system-scope
-//             store; the halfspace launch before it on the stream has completed, so its remote
-//             stores are done)
+//             store; the halfspace launch before it on the stream has completed, and each of its
+//             writing waves waited for the acknowledgement of its system-scope record stores
+//             before it ended, so every record is in every region)
 //   wait      every workgroup, lane j < n_ranks: poll flag[j] of the own region until >= g
 //             (system-scope loads of uncached memory: no cache can hold a stale flag), bounded by
 //             the 100 MHz realtime clock; a timeout sets the error word instead of hanging
 //   copy      every workgroup copies its slice of the gathered parity buffer into `out` (16-B
-//             loads of the uncached region, ordinary stores)
+//             nontemporal loads, which bypass L1, of the uncached region, which no L2 holds;
+//             ordinary stores)
 //   advance   the last workgroup to finish (a launch counter: every workgroup read the generation
 //             before it counted itself) resets the counter and stores the new generation
+// No cache-maintenance fence is needed on either side (each costs ~1.7 us on gfx950): the records
+// and flags live in uncached memory and move by system-scope / nontemporal accesses only, and the
+// generation and counter are read and written by atomics or across kernel boundaries.
 //
 // The grid is at most 64 workgroups of 256 threads; no workgroup waits on another of the launch
 // (each polls the flags itself), so residency does not matter.
@@ -44,7 +49,6 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
   const unsigned long long g = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
   const int64_t parity = static_cast<int64_t>(g & 1ull);
   if (blockIdx.x == 0 && tid < ps.n_ranks) {  // publish: this rank's rows are in every region
-    __atomic_thread_fence(__ATOMIC_RELEASE);  // (system scope: write back anything still dirty)
     __hip_atomic_store(flags_of(ps.region[tid], ps.rows) + ps.rank, g, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -60,7 +64,6 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
       __builtin_amdgcn_s_sleep(2);
     }
   }
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // (system scope: the records were written remotely)
   __syncthreads();
   // copy: the gathered parity buffer -> out, 16 B per thread per pass
   const dbl2* src = reinterpret_cast<const dbl2*>(ps.region[ps.rank] + parity * ps.rows * DRCVAR_OUT_WIDTH);
@@ -71,13 +74,12 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
     dst[i] = __builtin_nontemporal_load(src + i);
   // advance: the last workgroup out stores the generation
   __syncthreads();
-  if (tid == 0) {
-    __atomic_thread_fence(__ATOMIC_RELEASE);
-    const unsigned long long done = __hip_atomic_fetch_add(state + 1, 1ull, __ATOMIC_ACQ_REL,
+  if (tid == 0) {  // (g was read before this add: the poll loop above depends on its value)
+    const unsigned long long done = __hip_atomic_fetch_add(state + 1, 1ull, __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_AGENT);
     if (done + 1ull == gridDim.x) {
       __hip_atomic_store(state + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(state, g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

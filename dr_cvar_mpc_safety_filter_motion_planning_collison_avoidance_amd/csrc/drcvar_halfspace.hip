@@ -523,6 +523,9 @@ __device__ __forceinline__ void peer_store_record(const PeerArgs& pa, unsigned l
     store_sys(r + 6, gs);
     store_sys(r + 7, gt);
   }
+  // every record store acknowledged (system scope: performed in the destination's memory) before
+  // the wave ends, so the publish launch behind this one finds them all in place
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // d_i = h . xi_i — one expression, used both for the register-resident samples and for re-reads,
