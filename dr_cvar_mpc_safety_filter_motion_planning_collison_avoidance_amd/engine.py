@@ -95,7 +95,7 @@ def _typed(args):
     """Pre-convert an argument tuple to ctypes objects (saves the per-call conversion)."""
     out = []
     for a in args:
-        if isinstance(a, ctypes._SimpleCData):
+        if isinstance(a, (ctypes._SimpleCData, ctypes._Pointer)):   # (a pointer: a struct argument)
             out.append(a)
         elif isinstance(a, bool) or not isinstance(a, (int, float)):
             raise TypeError(f"unexpected argument {a!r}")

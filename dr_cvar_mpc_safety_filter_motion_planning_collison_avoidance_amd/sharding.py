@@ -125,7 +125,7 @@ class PeerExchange:
             ps.region[j] = regions[j]
         ps.rows, ps.state, ps.n_ranks, ps.rank = self.rows, self.state.data_ptr(), world, rank
         self.peers = ps
-        self._ps_ref = ctypes.byref(ps)
+        self._ps_ref = ctypes.pointer(ps)
         self._out_ptr = ctypes.c_void_p(self.out.data_ptr())
         self._spin = ctypes.c_int64(self.spin_limit_us)
 

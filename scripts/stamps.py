@@ -60,6 +60,17 @@ if os.environ.get("DRCVAR_STAMPS_REALTIME"):  # built with -DDRCVAR_STAMPS_REALT
     q = [0, 10, 50, 90, 100]
     print("  realtime (ns from the first unit's entry): entry percentiles",
           np.percentile(start, q).round(), " exit percentiles", np.percentile(end, q).round())
+    # the launch's occupancy over time (units in flight per 1 us bin): the ramp, the rounds, the tail
+    span = int(end.max()) + 1
+    edges = np.arange(0, span + 1000, 1000)
+    inflight = [int(((start < e1) & (end > e0)).sum()) for e0, e1 in zip(edges[:-1], edges[1:])]
+    print("  units in flight per us:", inflight)
+    peak = max(inflight)
+    full = [i for i, v in enumerate(inflight) if v >= 0.9 * peak]
+    print(f"  peak {peak} in flight; >= 90% of it from {full[0]} to {full[-1] + 1} us of {span / 1000:.1f} us;"
+          f" last entry {start.max() / 1000:.2f} us, first exit {end.min() / 1000:.2f} us,"
+          f" exits 50% {np.percentile(end, 50) / 1000:.2f}, 90% {np.percentile(end, 90) / 1000:.2f},"
+          f" 99% {np.percentile(end, 99) / 1000:.2f}, 100% {end.max() / 1000:.2f} us")
 else:
     print("  (phase cycles are per-XCD shader clocks; build with -DDRCVAR_STAMPS_REALTIME for the"
           " spread of entries/exits across workgroups)")

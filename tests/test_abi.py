@@ -132,3 +132,19 @@ def test_peer_exchange_host_side():
     assert peer(O=0) == _native.OK                                     # empty: nothing launched
     assert lib.drcvar_peer_alloc(0, ctypes.byref(ctypes.c_void_p()), out) == _native.ERR_INVALID_ARGUMENT
     assert lib.drcvar_peer_open(None, ctypes.byref(ctypes.c_void_p())) == _native.ERR_INVALID_ARGUMENT
+
+
+def test_prepared_peer_launch_takes_the_struct_pointer():
+    """sharding.PeerExchange.prepare_launch freezes a drcvar_peer_set* (a ctypes pointer) in the
+    argument tuple: the frozen call reaches the library's host-side checks (rows 7..11 > 4 rows)."""
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import engine
+    lib = _native.lib()
+    ps = _native.PeerSet()
+    ps.n_ranks, ps.rank, ps.rows, ps.state = 1, 0, 4, 16
+    ps.region[0] = 16
+    args = (ctypes.c_void_p(16), 1, 4, 10, 80, 20, 2, ctypes.c_void_p(16), 2, 0.3, 0.3, 0.2, 0.1, 0.15,
+            ctypes.pointer(ps), 7, ctypes.c_void_p(None), ctypes.c_void_p(None))
+    launch = engine.PreparedLaunch(lib.drcvar_safe_halfspaces_f64_peer, args, ())
+    with pytest.raises(_native.EngineError) as e:
+        launch()
+    assert e.value.code == _native.ERR_INVALID_ARGUMENT
