@@ -73,7 +73,8 @@ def solve(md, h, g, x0, xr, variant="base", tol=None, max_iter=60, trace=False, 
     wPl, lPl = np.maximum(c - md["pmin"], 1.0), np.full(2 * H, bl)
     if START.get("u_free", 0.0) > 0.0:       # the tracking optimum without rows, clipped to the box
         span = md["umax"] - md["umin"]
-        u = np.clip(-np.linalg.solve(md["H0"], f), md["umin"] + 0.05 * span, md["umax"] - 0.05 * span)
+        mg = START.get("u_margin", 0.05)
+        u = np.clip(-np.linalg.solve(md["H0"], f), md["umin"] + mg * span, md["umax"] - mg * span)
         pu = c + Gp @ u
         wUu, wUl = md["umax"] - u, u - md["umin"]
         wPu, wPl = np.maximum(md["pmax"] - pu, START.get("wp_floor", 1e-2)), np.maximum(pu - md["pmin"], START.get("wp_floor", 1e-2))

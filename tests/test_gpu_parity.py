@@ -102,6 +102,26 @@ def test_adversarial_distributions(kind):
                   cf.safe_halfspaces(samples, ego, 0.3, 0.3, 0.2, 0.1, 0.15))
 
 
+@pytest.mark.parametrize("n", [100, 1000, 2049, 3000, 4096, 4097, 5000, 5120, 8192, 10000, 16384])
+def test_all_equal_units_every_plan(n):
+    """Units whose samples are all one point (every obstacle's noise-free step 0,
+    simulation/obstacles.py:63) on every register plan — the 256-thread large plans settle them
+    from the moments' differ flag, the others from the register min/max or the exact fallback —
+    beside units where ONE sample differs (the first, i.e. the pivot; the last; one in the middle),
+    which must take the ordinary path: all against the closed form."""
+    T = 4
+    pts = np.array([[1.25, -0.5], [-3.0, 2.0], [0.1, 0.1], [7.5, -2.25]])
+    samples = np.repeat(pts[None, :, None, :], 4, axis=0).repeat(n, axis=2)   # [4, T, n, 2]
+    samples[1, :, 0, 0] += 0.5          # the pivot differs
+    samples[2, :, n - 1, 1] -= 0.25     # the last sample differs
+    samples[3, :, n // 2, 0] += 1e-9    # one sample in the middle, barely
+    ego = np.array([[-1.0, 0.3], [2.0, 2.0], [0.0, -4.0], [5.0, 5.0]])
+    got = _run(samples, ego, RiskParams())
+    want = cf.safe_halfspaces(samples, ego, 0.3, 0.3, 0.2, 0.1, 0.15)
+    _assert_match(got, want)
+    assert np.max(np.abs(got - want)) < 1e-12
+
+
 def test_non_finite_and_unbounded_sentinels():
     rng = np.random.default_rng(1)
     samples = rng.normal(size=(2, 3, 200, 2))
