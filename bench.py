@@ -264,7 +264,10 @@ class Stepper:
 
     def describe(self):
         backend = dist.get_backend() if dist.is_initialized() else None
-        coll = f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend})"
+        if getattr(self.sb, "peer", None) is not None:
+            coll = "peer-push exchange (records written into every rank's region by the kernel; publish/wait/copy launch)"
+        else:
+            coll = f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend})"
         parts = (["launch"] if self.compute else []) + ([coll] if self.exchange else [])
         what = " + ".join(parts)
         if self.fallback:

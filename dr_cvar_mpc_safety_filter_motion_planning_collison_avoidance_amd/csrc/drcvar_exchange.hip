@@ -20,8 +20,8 @@
 // and flags live in uncached memory and move by system-scope / nontemporal accesses only, and the
 // generation and counter are read and written by atomics or across kernel boundaries.
 //
-// The grid is at most 64 workgroups of 256 threads; no workgroup waits on another of the launch
-// (each polls the flags itself), so residency does not matter.
+// The grid is at most 256 workgroups of 256 threads (one per 4 K records); no workgroup waits on
+// another of the launch (each polls the flags itself), so residency does not matter.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -32,7 +32,8 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int64_t kMaxGroups = 64;  // 64 x 4 KB per pass: C5's 819 KB in 4 passes
+constexpr int kPerThread = 4;         // 16-B copies per thread, their loads issued together
+constexpr int64_t kMaxGroups = 256;   // C5 (12 800 records, 819 KB): 50 workgroups, one pass
 constexpr int64_t kFlagsDoubles = 64;  // the flag slot of a region (512 B: room for 64 ranks)
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
@@ -65,13 +66,25 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
     }
   }
   __syncthreads();
-  // copy: the gathered parity buffer -> out, 16 B per thread per pass
+  // copy: the gathered parity buffer -> out, kPerThread 16-B loads in flight per thread per pass
+  // (the uncached region answers from HBM: one round trip per pass, not per element)
   const dbl2* src = reinterpret_cast<const dbl2*>(ps.region[ps.rank] + parity * ps.rows * DRCVAR_OUT_WIDTH);
   dbl2* dst = reinterpret_cast<dbl2*>(out);
   const int64_t n2 = ps.rows * DRCVAR_OUT_WIDTH / 2;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + tid; i < n2;
-       i += static_cast<int64_t>(gridDim.x) * kThreads)
-    dst[i] = __builtin_nontemporal_load(src + i);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kThreads + tid; i0 < n2; i0 += stride * kPerThread) {
+    dbl2 v[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int64_t i = i0 + k * stride;
+      if (i < n2) v[k] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int64_t i = i0 + k * stride;
+      if (i < n2) dst[i] = v[k];
+    }
+  }
   // advance: the last workgroup out stores the generation
   __syncthreads();
   if (tid == 0) {  // (g was read before this add: the poll loop above depends on its value)
@@ -155,7 +168,7 @@ int drcvar_peer_signal_wait(const drcvar_peer_set* peers, double* out, int64_t s
                             void* stream) {
   if (!valid(peers) || !out || spin_limit_us <= 0) return DRCVAR_ERR_INVALID_ARGUMENT;
   const int64_t n2 = peers->rows * DRCVAR_OUT_WIDTH / 2;
-  int64_t groups = (n2 + kThreads - 1) / kThreads;
+  int64_t groups = (n2 + kThreads * kPerThread - 1) / (kThreads * kPerThread);
   groups = groups < 1 ? 1 : (groups > kMaxGroups ? kMaxGroups : groups);
   (void)hipGetLastError();
   hipLaunchKernelGGL(peer_signal_wait_kernel, dim3(static_cast<unsigned>(groups)), dim3(kThreads), 0,
