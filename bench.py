@@ -54,6 +54,9 @@ from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.engine imp
 # all-gather is latency-bound (~123 KB), two chunks at most; C5's shard kernel is long enough
 # (~40 us at 8 ranks) to hide a chunk's gather behind the next chunk's kernel
 CHUNKS = {"c2": [2], "c3": [2], "c4": [2], "c5": [2, 4]}
+# bound of one peer-exchange wait in the strong legs: a step waits at most for a slower rank's
+# kernel (~0.3 ms at C5 on one GPU); a wait that gives up sets the error word and the form is dropped
+PEER_SPIN_US = 200_000
 WORKLOADS = {
     # name: (obstacles, steps, samples, description)
     "c2": (4, 20, 1000, "multi_obstacle-like synthetic, 4 obstacles, T=20, N=1000 (BASELINE config 2)"),
@@ -482,9 +485,14 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload,
     sb = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed, gather_device=gdev)
     K = args.strong_steps
 
-    def run_form(sbx):
+    def run_form(sbx, warm_check=None):
         st = Stepper(sbx, mode, 10, K, dev, world=world, ctrl=ctrl)
         st.run(min(K, 10))
+        if warm_check is not None:   # (rank-agreed) a form that failed its warm-up is not timed
+            torch.cuda.synchronize(dev)
+            why = warm_check()
+            if not agree(world, ctrl, why is None):
+                return None, why or "failed its warm-up on another rank"
         el, _, _ = timed(world, lambda: st.run(K), dev, stream)
         return el, st.describe()
 
@@ -530,11 +538,19 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload,
         if args.exchange in ("auto", "peer"):   # (gloo rehearsal too: ranks sharing one GPU map each other)
             try:
                 sbp = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed,
-                                            exchange="peer", ctrl=ctrl, samples=sb.samples)
+                                            exchange="peer", ctrl=ctrl, samples=sb.samples,
+                                            peer_spin_us=PEER_SPIN_US)
             except sharding.PeerExchangeUnavailable as exc:
                 exchanges["peer"] = {"unavailable": str(exc)}
-            else:
-                el_p, launch_p = run_form(sbp)
+                sbp = None
+            if sbp is not None:
+                el_p, launch_p = run_form(sbp, lambda: (None if sbp.peer.error() == 0 else
+                                                        f"a wait gave up (error word {sbp.peer.error():#x})"))
+            if sbp is not None and el_p is None:
+                exchanges["peer"] = {"unavailable": launch_p}
+                sbp.close()
+                sbp = None
+            if sbp is not None:
                 err = sbp.peer.error()
                 same = err == 0 and bool(torch.equal(sbp.records().to(ref.device), ref))
                 same = agree(world, ctrl, same)

@@ -863,7 +863,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   constexpr bool kPilot = P <= 8;
   __shared__ double2 pilot[kPilot ? kWave : 1];
   __shared__ double red_mom[2 * NW];
-  __shared__ float red_mom0[6 * NW];
+  __shared__ float red_mom0[5 * NW];
   __shared__ double red_rng[2 * NW];
   __shared__ double red_tail[NW];
 
@@ -935,24 +935,14 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   // row 0 only (the first BLOCK samples), shifted by the unit's first sample and summed in fp32 —
   // they merely position the fast-path window, so a subsample at low precision is enough: an
   // inaccurate window can only cost speed (the exact fallback), never exactness.
-  // The 256-thread large plans also flag the samples that differ from the pivot (mom0[5], reduced
-  // with the moments): zero means every sample of the unit is the same point — the noise-free step
-  // 0 of every obstacle (simulation/obstacles.py:63) — and the unit is settled right after
-  // barrier 1's sums instead of by the exact fallback, whose re-reads made these the slowest units
-  // of a C4 launch (stamps: ~23 us against a ~10 us median; its last wave waited on their CUs).
-  // (Not in the 512 / 1024-thread plans: the flag takes the 512 x 20 plan from 127 to 130 VGPRs,
-  // i.e. from two workgroups per CU to one; C5's 12.5 waves of units hide its slow units.)
-  constexpr bool kSettleEqual = !kPilot && BLOCK <= 256;
   double mom[2] = {0.0, 0.0};               // Sx Sy
-  float mom0[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // row 0, pivot-shifted: Sa Sb Saa Sbb Sab; + differing
-  bool differ = false;  // (a lane mask: no vector register)
+  float mom0[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // row 0, pivot-shifted: Sa Sb Saa Sbb Sab
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const bool valid = tid + j * BLOCK < n;
     const double a = valid ? x[j] : 0.0, b = valid ? y[j] : 0.0;
     mom[0] += a;
     mom[1] += b;
-    if constexpr (kSettleEqual) differ = differ || (valid && (x[j] != px || y[j] != py));
     if (!kPilot && j == 0) {
       const float fa = valid ? static_cast<float>(x[0] - px) : 0.f;
       const float fb = valid ? static_cast<float>(y[0] - py) : 0.f;
@@ -963,7 +953,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
       mom0[4] = fa * fb;
     }
   }
-  if constexpr (kSettleEqual) mom0[5] = differ ? 1.f : 0.f;
   if (kPilot && wave == 0) pilot[lane] = make_double2(x[0], y[0]);  // samples 0..63 (lane < n)
   DRCVAR_STAMP(1);
   DRCVAR_STAMP_WAVE(0);  // diagnostic build: this wave's samples summed (its loads done)
@@ -971,7 +960,7 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
   if constexpr (kPilot)
     block_sum_moments<NW, 2, 0, true>(mom, mom0, red_mom, red_mom0, pilot, &pv);  // [barrier 1]
   else
-    block_sum_moments<NW, 2, kSettleEqual ? 6 : 5>(mom, mom0, red_mom, red_mom0);  // [barrier 1]
+    block_sum_moments<NW, 2, 5>(mom, mom0, red_mom, red_mom0);           // [barrier 1]
   DRCVAR_STAMP(2);
   const double mux = mom[0] * inv_n, muy = mom[1] * inv_n;
   // any non-finite sample makes a sum non-finite (so do sums that overflow): solver failure
@@ -1148,13 +1137,6 @@ safe_halfspace_kernel(const double* __restrict__ samples, int64_t n_steps, int n
     // Small plans only: on the 20-sample plan the extra live range costs the second workgroup
     // per CU (127 -> 130 VGPRs), and a C5 launch is bandwidth-bound, not set by its slowest unit.
     bool settled = false;
-    if constexpr (kSettleEqual) {
-      if (mom0[5] == 0.f) {  // uniform: every sample is the unit's first (bitwise its d, no tail)
-        tau = project(h0, h1, px, py);
-        dsum = 0.0;
-        settled = true;
-      }
-    }
     if (P <= 8 && !(var_d > 0.0)) {  // uniform
       double lo[1] = {INFINITY}, hi[1] = {-INFINITY};
 #pragma unroll

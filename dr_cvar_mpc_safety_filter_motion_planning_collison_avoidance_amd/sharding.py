@@ -368,7 +368,7 @@ class ShardedBatch:
                  stream_offset: int = 0, noise_cov=None, zero_first_step: bool = True,
                  gather_device=None, chunks: int = 1, force_exchange: bool = False,
                  exchange: str = "rccl", ctrl=None, sample_fn=None, prepare_fn=None,
-                 samples: torch.Tensor | None = None):
+                 samples: torch.Tensor | None = None, peer_spin_us: int = 2_000_000):
         from .simulation import obstacles
         if exchange not in ("rccl", "peer"):
             raise ValueError(f"exchange must be 'rccl' or 'peer', not {exchange!r}")
@@ -405,7 +405,8 @@ class ShardedBatch:
         self.peer = None
         self.scratch = None
         if do_exchange and exchange == "peer":
-            self.peer = PeerExchange(self.per * world_size, world_size, rank, dev, ctrl=ctrl)
+            self.peer = PeerExchange(self.per * world_size, world_size, rank, dev, ctrl=ctrl,
+                                     spin_limit_us=peer_spin_us)
             self.full = self.peer.out
         else:
             self.full = (torch.empty((self.per * world_size, engine.OUT_WIDTH), dtype=torch.float64,
