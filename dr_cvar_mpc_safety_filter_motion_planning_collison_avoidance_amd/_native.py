@@ -102,6 +102,8 @@ EXPORTED_SYMBOLS = (
     "drcvar_peer_open",
     "drcvar_peer_close",
     "drcvar_peer_can_access",
+    "drcvar_peer_bus_id",
+    "drcvar_peer_device_of",
     "drcvar_peer_signal_wait",
     "drcvar_safe_halfspaces_f64_peer",
 )
@@ -315,6 +317,10 @@ def _bind(lib):
     lib.drcvar_peer_close.restype = ctypes.c_int
     lib.drcvar_peer_can_access.argtypes = [i32, i32, i32p]
     lib.drcvar_peer_can_access.restype = ctypes.c_int
+    lib.drcvar_peer_bus_id.argtypes = [i32, ctypes.c_char_p, i32]
+    lib.drcvar_peer_bus_id.restype = ctypes.c_int
+    lib.drcvar_peer_device_of.argtypes = [ctypes.c_char_p, i32p]
+    lib.drcvar_peer_device_of.restype = ctypes.c_int
     lib.drcvar_peer_signal_wait.argtypes = [peerp, ptr, i64, ptr]
     lib.drcvar_peer_signal_wait.restype = ctypes.c_int
     lib.drcvar_safe_halfspaces_f64_peer.argtypes = [

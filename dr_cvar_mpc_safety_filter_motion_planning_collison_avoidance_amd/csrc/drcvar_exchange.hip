@@ -164,6 +164,19 @@ int drcvar_peer_can_access(int32_t device, int32_t peer_device, int32_t* can_acc
   return DRCVAR_OK;
 }
 
+int drcvar_peer_bus_id(int32_t device, char* bus_id, int32_t len) {
+  if (!bus_id || len < 13 || device < 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  return hipDeviceGetPCIBusId(bus_id, len, device) == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
+}
+
+int drcvar_peer_device_of(const char* bus_id, int32_t* device) {
+  if (!bus_id || !device) return DRCVAR_ERR_INVALID_ARGUMENT;
+  int d = -1;
+  if (hipDeviceGetByPCIBusId(&d, bus_id) != hipSuccess || d < 0) return DRCVAR_ERR_UNSUPPORTED;
+  *device = d;
+  return DRCVAR_OK;
+}
+
 int drcvar_peer_signal_wait(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us,
                             void* stream) {
   if (!valid(peers) || !out || spin_limit_us <= 0) return DRCVAR_ERR_INVALID_ARGUMENT;

@@ -83,7 +83,10 @@ class PeerExchange:
             rc = lib.drcvar_peer_alloc(doubles, ctypes.byref(self._own), handle)
         ok = rc == _native.OK
         why = None if ok else f"rank {rank}: drcvar_peer_alloc -> {rc}"
-        mine = (bytes(handle), device.index if ok else -1)
+        bus = ctypes.create_string_buffer(64)
+        if ok and lib.drcvar_peer_bus_id(device.index, bus, 64) != _native.OK:
+            ok, why = False, f"rank {rank}: no PCI bus id for device {device.index}"
+        mine = (bytes(handle), bus.value.decode() if ok else "")
         infos = [None] * world
         if world > 1:
             dist.all_gather_object(infos, mine, group=ctrl)
@@ -92,13 +95,18 @@ class PeerExchange:
         regions = [None] * world
         if ok:
             regions[rank] = self._own.value
-            for j, (h, d) in enumerate(infos):
+            for j, (h, pbus) in enumerate(infos):
                 if j == rank:
                     continue
-                can = ctypes.c_int32(0)
-                if d < 0 or lib.drcvar_peer_can_access(device.index, d, ctypes.byref(can)) != _native.OK \
+                # the peer's GPU by its bus id, in this process's device numbering (the ranks' lists
+                # of visible devices may differ); same device: the one-GPU rehearsal
+                d, can = ctypes.c_int32(-1), ctypes.c_int32(0)
+                if not pbus or lib.drcvar_peer_device_of(pbus.encode(), ctypes.byref(d)) != _native.OK:
+                    ok, why = False, f"rank {rank}: rank {j}'s GPU {pbus or '?'} is not visible here"
+                    break
+                if lib.drcvar_peer_can_access(device.index, d.value, ctypes.byref(can)) != _native.OK \
                         or not can.value:
-                    ok, why = False, f"rank {rank}: device {device.index} cannot access rank {j}'s device {d}"
+                    ok, why = False, f"rank {rank}: device {device.index} cannot access rank {j}'s GPU {pbus}"
                     break
                 r = ctypes.c_void_p()
                 with torch.cuda.device(device):

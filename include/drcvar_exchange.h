@@ -12,8 +12,8 @@
  * an ordinary device buffer.  No collective library, no host round trip; graph-capturable.
  *
  * Region of a rank (uncached device memory, drcvar_peer_alloc; doubles):
- *   [0, rows*8)              records of the odd steps' parity 0 ... (parity = generation & 1)
- *   [rows*8, 2*rows*8)       records of parity 1
+ *   [0, rows*8)              records of the steps of even generation (parity = generation & 1)
+ *   [rows*8, 2*rows*8)       records of the steps of odd generation
  *   [2*rows*8, +64)          flags: uint64 per source rank, the last generation it finished
  * rows = n_ranks * per (per = units of one rank's block, the tail rank padded), record r at
  * r*8 in the [O*T, 8] order of drcvar_safe_halfspaces_f64 (DRCVAR_COL_*).
@@ -61,6 +61,12 @@ int drcvar_peer_open(const void* handle, double** region);
 int drcvar_peer_close(double* region);
 /* Whether `device` can access `peer_device`'s memory directly (1 for the same device). Host-only. */
 int drcvar_peer_can_access(int32_t device, int32_t peer_device, int32_t* can_access);
+/* The PCI bus id of `device` (host string, at most `len` bytes with the terminator), and the device
+   of this process that has a given bus id (DRCVAR_ERR_UNSUPPORTED when this process does not see
+   it): ranks name their GPUs to each other by bus id, since device indices differ between
+   processes whose visible-device lists differ.  Host-only. */
+int drcvar_peer_bus_id(int32_t device, char* bus_id, int32_t len);
+int drcvar_peer_device_of(const char* bus_id, int32_t* device);
 
 /* The step's publish + wait + copy (one launch on `stream`): out[rows * 8] doubles. */
 int drcvar_peer_signal_wait(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us,

@@ -20,6 +20,10 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:?outdir}; shift; mkdir -p $OUT
 MPC_SHAPES=${MPC_SHAPES:-"npz:tests/golden/qp_c5_degenerate.npz npz:tests/golden/qp_h30_straggler.npz 50,256,1 50,256,3 30,3,1024 20,10,3 30,3,1"}
 CMD="python3 bench.py --gpus 1 --steps 20 --warmup 5"
+# counter passes go through an input file: rocprofv3 then runs the program as a child process
+# (with --pmc on the command line its launcher replaces itself by the program after touching the
+# GPU, which the box refuses and reports)
+pmcfile() { local f=$OUT/pmc_$(echo "$*" | tr ' ' '_').txt; echo "pmc: $*" > $f; echo $f; }
 fail() { echo "stopping: $1"; exit ${2:-2}; }
 for s in "$@"; do
   echo "=== $s ($(date +%T))"
@@ -55,14 +59,14 @@ for s in "$@"; do
       done
       grep -h "total\|P1 span\|solves (ipm)\|exchanges \|factor" $OUT/stamps_*.log ;;
     kernel_time)
-      timeout -s KILL 600 rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE --kernel-trace -d $OUT/busy -o run --output-format csv \
-        -- $CMD > $OUT/busy_bench.json 2> $OUT/busy_bench.err || fail kernel_time
+      timeout -s KILL 600 rocprofv3 -i $(pmcfile GRBM_COUNT GRBM_GUI_ACTIVE) --kernel-trace -d $OUT/busy -o run \
+        --output-format csv -- $CMD > $OUT/busy_bench.json 2> $OUT/busy_bench.err || fail kernel_time
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv \
         -- $CMD > $OUT/trace_bench.json 2> $OUT/trace_bench.err || fail kernel_time ;;
     pmc)
       for w in c3 c4 c5; do
         for k in FETCH_SIZE WRITE_SIZE; do
-          timeout -s KILL 600 rocprofv3 --pmc $k -d $OUT/pmc_${k}_$w -o run --output-format csv -- python3 bench.py \
+          timeout -s KILL 600 rocprofv3 -i $(pmcfile $k) -d $OUT/pmc_${k}_$w -o run --output-format csv -- python3 bench.py \
             --workload $w --steps 20 --warmup 2 --graph-batch 10 --no-large --no-cpu-baseline > $OUT/pmc_${k}_$w.log 2>&1 || fail pmc
         done
         python3 scripts/pmc_traffic.py $w $OUT/pmc_FETCH_SIZE_$w $OUT/pmc_WRITE_SIZE_$w || fail pmc

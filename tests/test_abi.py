@@ -111,6 +111,8 @@ def test_peer_exchange_host_side():
     can = ctypes.c_int32(0)
     assert lib.drcvar_peer_can_access(0, 0, ctypes.byref(can)) == _native.OK and can.value == 1
     assert lib.drcvar_peer_can_access(-1, 0, ctypes.byref(can)) == _native.ERR_INVALID_ARGUMENT
+    assert lib.drcvar_peer_bus_id(0, ctypes.create_string_buffer(8), 8) == _native.ERR_INVALID_ARGUMENT
+    assert lib.drcvar_peer_device_of(None, ctypes.byref(can)) == _native.ERR_INVALID_ARGUMENT
     ps = _native.PeerSet()
     ps.n_ranks, ps.rank, ps.rows, ps.state = 2, 0, 10, 16
     ps.region[0] = 16
