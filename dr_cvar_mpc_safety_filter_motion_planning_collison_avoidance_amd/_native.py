@@ -175,13 +175,29 @@ def _quoted_includes(path: str, seen=None) -> list:
 
 
 _toolchain_id = None
+TOOLCHAIN_PATH = os.path.join(LIB_DIR, "toolchain.id")
 
 
-def _toolchain() -> bytes:
-    """``hipcc --version`` (the compiler's identity: part of every object key and source key)."""
+def _toolchain(probe: bool = False) -> bytes:
+    """The compiler's identity (``hipcc --version``): part of every object key and source key.
+    build() probes hipcc (probe=True) and records the answer next to the library it links;
+    everything else reads that record — the identity of the compiler that built the loaded
+    library — and never starts a process: bench.py asks for source_key() after the GPU is
+    initialised, where forking a child to exec hipcc is not allowed."""
     global _toolchain_id
-    if _toolchain_id is None:
-        _toolchain_id = subprocess.run(["hipcc", "--version"], capture_output=True, check=True).stdout
+    if probe:
+        tid = subprocess.run(["hipcc", "--version"], capture_output=True, check=True).stdout
+        os.makedirs(LIB_DIR, exist_ok=True)
+        with open(TOOLCHAIN_PATH + ".tmp", "wb") as f:
+            f.write(tid)
+        os.replace(TOOLCHAIN_PATH + ".tmp", TOOLCHAIN_PATH)
+        _toolchain_id = tid
+    elif _toolchain_id is None:
+        try:
+            with open(TOOLCHAIN_PATH, "rb") as f:
+                _toolchain_id = f.read()
+        except OSError:
+            return b"unrecorded (library not built)"
     return _toolchain_id
 
 
@@ -222,7 +238,7 @@ def build(verbose: bool = False, extra_flags=()) -> str:
     incs = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.inc")))  # tables the sources include
     headers = b"".join(open(h, "rb").read() for h in HEADERS + incs)
     # the compiler's identity is part of every key: objects of an older hipcc / ROCm are rebuilt
-    toolchain = _toolchain()
+    toolchain = _toolchain(probe=True)
     objs, procs = [], []
     for src, defs in _compile_units():
         flags = _unit_flags(defs, extra_flags)
