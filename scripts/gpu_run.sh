@@ -14,6 +14,7 @@
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of c3 c4 c5 (profiles/pmc_traffic.json)
 #   sampler      scripts/micro/sampler_bench.py (VARIANTS as for mpc)
 #   dist         scripts/gpu_dist.sh (gloo, 2 and 4 ranks sharing cuda:0)
+#   shard        scripts/micro/shard_kernel_times.py (per-rank shard kernels of the strong legs)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -79,6 +80,9 @@ for s in "$@"; do
       grep -H . $OUT/sampler_*.log | grep -v amdgpu ;;
     dist)
       OUTDIR=$OUT timeout -k 10 1000 bash scripts/gpu_dist.sh || fail dist ;;
+    shard)
+      timeout -k 10 300 python3 scripts/micro/shard_kernel_times.py > $OUT/shard_kernel_times.json 2> $OUT/shard.err \
+        || { tail $OUT/shard.err; fail shard; } ;;
     *) fail "unknown step $s" ;;
   esac
 done

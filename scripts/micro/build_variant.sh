@@ -5,7 +5,8 @@
 # DRCVAR_DIAG_LIB runs.  The product sources carry only the stamp hooks; the other diagnostic
 # switches (-DDRCVAR_DIAG_STAGE, -DDRCVAR_NO_PIPE, -DDRCVAR_POLISH_RHO, -DDRCVAR_NT_BYTES,
 # -DDRCVAR_HS_LDS_PAD, -DDRCVAR_SAMPLER_NO_STORE) live in patches/diag_switches.diff, applied here
-# to a temporary copy of the sources.
+# to a temporary copy of the sources; PATCHES="<a.diff> ..." applies more (e.g.
+# patches/early_polish_knobs.diff: the early polish's thresholds as -D switches).
 set -eu
 cd "$(dirname "$0")/../.."
 name=$1; src=$2; shift 2
@@ -15,6 +16,7 @@ tmp=$(mktemp -d)
 trap 'rm -rf $tmp' EXIT
 cp $PKG/csrc/*.hip $PKG/csrc/*.inc $tmp/
 patch -s -p1 -d $tmp < scripts/micro/patches/diag_switches.diff
+for p in ${PATCHES:-}; do patch -s -p1 -d $tmp < $p; done
 new=()
 if [ "$src" = drcvar_mpc ]; then
   for k in 0 1 2 3 4; do
