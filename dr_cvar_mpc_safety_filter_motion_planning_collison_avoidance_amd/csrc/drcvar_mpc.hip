@@ -155,14 +155,21 @@ constexpr double kPolishRho = 1e6;    // method-of-multipliers penalty of the po
 constexpr int kPolishIters = 12;      // multiplier passes per active-set guess
 constexpr int kPolishAttempts = 6;    // active-set corrections
 constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close to the optimum
-// early polish (round 5): a first round whose merit is <= kEarlyPolishMerit but fell less than
-// tenfold over the last two iterations is stalled by weakly active rows (w and lambda of a pair
-// both heading to zero: the Mehrotra steps alternate long and short; the straggler of
-// tests/golden/qp_h30_straggler.npz took 20 iterations against a batch mean of 5.3), so it
-// polishes from there; a polish that fails resumes the interior-point method to the tolerance
-constexpr double kEarlyPolishMerit = 1e-3;
-constexpr double kStallRatio = 0.1;
-constexpr int kEarlyPolishAttempts = 2;  // active-set corrections of an early polish
+// early polish (round 6): the first round polishes as soon as its merit is <= kEarlyPolishMerit,
+// from the predictor's active-set guess at that iterate, with at most kEarlyPolishAttempts
+// corrections; the polish certifies itself (sign conditions and equality residuals), and one that
+// fails restores the iterate and resumes the interior-point method to the tolerance.  Round 5 did
+// this only on a stall (merit fallen less than tenfold over two iterations: the straggler of
+// tests/golden/qp_h30_straggler.npz); polishing every problem from 1e-2 instead of iterating to
+// tol = 1e-7 first (scripts/micro/patches/early_polish_knobs.diff, interleaved on one box,
+// profiles/r06/early_polish/): the C5 fixture 10 -> 8 iterations, 0.574 -> 0.478 ms; main.py's
+// mean filter 15 -> 12, 0.785 -> 0.681 ms; the straggler 11 -> 7; 1 024 distinct problems 0.405 ->
+// 0.341 ms (mean 5.3 -> 3.3 iterations); every problem optimal and polished, |u - oracle| <= 7e-10.
+// From 3e-2 the guess failed on the mean filter (three attempts, then the resume: 1.02 ms); with
+// two attempts from 1e-2 one problem of the 1 024 needed the resume (0.420 ms); 1e-3 / 3e-3 /
+// 1e-4 polish one or two iterations later.
+constexpr double kEarlyPolishMerit = 1e-2;
+constexpr int kEarlyPolishAttempts = 3;  // active-set corrections of an early polish
 constexpr double kPolishDualTol = 1e-7;
 constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
 constexpr double kStartMuMany = 20.0;   // barrier parameter of the starting point, >= 64 obstacles
@@ -2243,7 +2250,6 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
   // one round: P1 of the current iterate, the interior-point loop, the polish; true when a resume
   // round should follow.  Inlined at both call sites (a loop around it, or an out-of-line
   // function, made the compiler spill inside the interior-point loop: C5 QP +5 % / +40 %).
-  double merit_back1 = kHuge, merit_back2 = kHuge;  // the merit one and two iterations back
   bool early = false;  // the first round left for an early polish (kEarlyPolishMerit)
   auto ipm_round = [&](const int round) __attribute__((always_inline)) -> bool {
   bool converged = false;  // this round's loop met its tolerance (the factorisation beside it stands)
@@ -2370,7 +2376,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         best_merit = merit;
         break;
       }
-      if (round == 0 && a.polish && merit <= kEarlyPolishMerit && merit > kStallRatio * merit_back2) {
+      if (round == 0 && a.polish && merit <= kEarlyPolishMerit) {
         converged = true;  // (the factorisation beside this P1 serves the active-set guess)
         early = true;
         // the best iterate is this one (u, merit and iteration together): the post-loop restore
@@ -2380,8 +2386,6 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         for (int j = tid; j < n; j += kBlock) best_u[j] = s.u[j];
         break;
       }
-      merit_back2 = merit_back1;
-      merit_back1 = merit;
       if (merit < best_merit) {  // uniform: every thread holds the same merit
         best_merit = merit;
         best_it = it;

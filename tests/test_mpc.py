@@ -693,7 +693,8 @@ def test_gpu_h30_straggler_matches_oracle(dev):
 def test_gpu_c5_mean_filter_matches_oracle(dev):
     """The C5 mean-metric filter (tests/golden/qp_c5_mean.npz) on the clustered form and on one
     workgroup: optimal, polished, within MPC_TOL of the oracle, objective to 1e-9, and no more
-    interior-point iterations than the round-5 kernel took (15)."""
+    interior-point iterations than the round-6 kernel takes (12: the early polish from merit
+    1e-2; the round-5 kernel took 15, kernel_iterations_r05)."""
     import torch
     from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core import mpc_filter as mf
     z, _ = _c5_mean()
@@ -708,7 +709,7 @@ def test_gpu_c5_mean_filter_matches_oracle(dev):
         info = info[0].cpu().numpy()
         assert int(info[_native.MPC_INFO_STATUS]) == _native.MPC_STATUS_OPTIMAL, info
         assert info[_native.MPC_INFO_POLISHED] == 1, info
-        assert info[_native.MPC_INFO_ITERATIONS] <= float(z["kernel_iterations_r05"]), info
+        assert info[_native.MPC_INFO_ITERATIONS] <= min(12.0, float(z["kernel_iterations_r05"])), info
         np.testing.assert_allclose(u[0].cpu().numpy(), z["u_expected"], atol=MPC_TOL)
         np.testing.assert_allclose(x[0].cpu().numpy(), z["x_expected"], atol=MPC_TOL)
         assert abs(info[_native.MPC_INFO_OBJECTIVE] - float(z["objective"])) <= 1e-9 * float(z["objective"])
@@ -716,7 +717,7 @@ def test_gpu_c5_mean_filter_matches_oracle(dev):
 
 @pytest.mark.gpu
 def test_gpu_failed_early_polish_resumes_to_the_oracle(dev):
-    """The straggler leaves its first round by the early polish (a stall at merit <= 1e-3);
+    """The straggler leaves its first round by the early polish (merit <= 1e-2);
     options.debug_force_resume makes that polish give up at once, so the solve resumes the
     interior-point method from the early iterate (its u, slacks and duals together) to the normal
     tolerance and polishes there: the answer must still be the oracle's, alone and in a 160-problem
