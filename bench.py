@@ -425,7 +425,7 @@ def main():
                                       args, elapsed / K),
             "strong_scaling": strong,
         }
-    large = mpc = sampling = None
+    large = mpc = sampling = replicated = None
     c5leg = (strong or {}).get("c5")
     if rank == 0 and world == 1 and not args.no_large and c5leg is not None:
         big = c5leg.pop("_batch")
@@ -436,11 +436,13 @@ def main():
                               params, with_cpu=not args.no_cpu_baseline)
         del big
         torch.cuda.empty_cache()
+        replicated = c3_replicated(dev, stream, params)
     for leg in (strong or {}).values():
         leg.pop("_batch", None)
         leg.pop("_roofline", None)
     if rank == 0:
         result["roofline_large"] = large
+        result["roofline_c3_replicated"] = replicated
         result["mpc_handoff"] = mpc
         result["sampling"] = sampling
         if world == 1 and not args.no_cpu_baseline:
@@ -678,6 +680,41 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload,
         large["timing"] = f"HIP events over {K} graph-replayed launches (replays of 10)"
         out["_roofline"] = large
     sb.close()   # collective for the peer exchange (every rank chose the same form); else a no-op
+    return out
+
+
+def c3_replicated(dev, stream, params, copies=640, reps=20, check_obstacles=100):
+    """BASELINE.md §3's second roofline convention: the metric's C3 batch (10 obstacles x T=20 x
+    N=1000, the 256x4 launch plan) replicated to a >= 2 GB working set — `copies` C3 scenes sharing
+    the ego path, one launch over all of them (6 400 obstacles, 128 000 units, 2.06 GB resident) —
+    graph-replayed, HIP events.  The metric line's C3 step is one 3.2 MB launch (latency- and
+    dispatch-bound); this is the same kernel plan where bandwidth, not the dispatch, bounds it.
+    Offsets of the first `check_obstacles` obstacles are checked against the C oracle after timing."""
+    import numpy as np
+    O, T, N, _ = WORKLOADS["c3"]
+    O *= copies
+    nominal = synthetic.nominal_paths(O, T, dev, seed=5)
+    ego = synthetic.straight_line_ego(T, dev)
+    sb = sharding.ShardedBatch(nominal, ego, N, params, 1, 0, seed=5)
+    st = Stepper(sb, "graph", 10, reps, dev, exchange=False)
+    st.run(10)
+    _, ks, _ = timed(1, lambda: st.run(reps), dev, stream)
+    ks /= reps
+    out = roofline(sb.algorithmic_bytes, ks, None)
+    out.update({"workload": f"{copies} x C3 (10 obstacles x {T} steps x {N} samples) = {O} obstacles, "
+                            f"{sb.U} units, {sb.algorithmic_bytes / 1e9:.2f} GB resident, one launch",
+                "halfspaces_per_s": sb.U / ks,
+                "timing": f"HIP events over {reps} graph-replayed launches (replays of 10)"})
+    from oracle import c_oracle
+    s = sb.samples.view(O, T, N, 2)[:check_obstacles].cpu().numpy()
+    ref = c_oracle.safe_halfspaces(s, ego.cpu().numpy(), params.robot_radius, params.obstacle_radius,
+                                   params.alpha, params.delta, params.epsilon,
+                                   nthreads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    got = sb.records().view(O, T, -1)[:check_obstacles].cpu().numpy()
+    out["max_abs_err"] = float(np.max(np.abs(got[..., [2, 5, 6, 7]] - ref[..., [2, 5, 6, 7]])))
+    out["checked"] = f"obstacles [0, {check_obstacles}) x {T} steps against oracle/drcvar_oracle.c"
+    del st
+    sb.close()
     return out
 
 

@@ -21,7 +21,10 @@ is not reproducible in parallel, so the device generator defines its own: for th
 log1p series; 512 table angles + short sin / cos series) with the kernel's own tables, read from
 ``csrc/drcvar_sampling_tables.inc``, so the tests can check them against extended-precision
 references and the kernel against this mirror.  The kernel contracts its polynomial steps into
-FMAs; numpy rounds each product, so the two agree to a few ulp, not bit for bit.
+FMAs, and for an isotropic covariance ``l^2 I`` it computes ``l^2 (-2 log u)`` (the scale carried
+by the log's coefficients and table, ``csrc/drcvar_generator.inc``) and adds ``sqrt`` of that times
+(cos, sin) to the nominal point, where this mirror forms ``nominal + L z``; numpy rounds each
+product, so the two agree to a few ulp, not bit for bit.
 """
 from __future__ import annotations
 

@@ -262,6 +262,35 @@ def test_device_sampler_large_batch_paths(dev):
     del whole, flat
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cov", ["iso", "full"])
+def test_device_sampler_full_blocks_repeatable_and_mirrored(dev, cov):
+    """The full-block store path (every pair of a workgroup's range in the unit: no per-pair test)
+    on a batch above the MALL (nontemporal stores), for the isotropic covariance (the scale rides in
+    the log) and a full one: two refills into buffers pre-filled with different values are bitwise
+    equal (a store-data hazard once corrupted a few hundred samples per refill at random,
+    scripts/micro/sampler_check.py), every sample is written, and full-block units match the
+    NumPy mirror and the ordinary-store unit-range draws."""
+    import torch
+    from oracle import philox_sampler as ps
+    O, T, N = 64, 50, 10001                      # odd N: the last workgroup of a unit takes the checked loop
+    c = ob.NOISE_COV if cov == "iso" else np.array([[0.04, 0.012], [0.012, 0.02]])
+    nom = _nominal(dev, O, T)
+    a = torch.full((O, T, N, 2), 7.0, dtype=torch.float64, device=dev)
+    b = torch.full((O, T, N, 2), -7.0, dtype=torch.float64, device=dev)
+    ob.sample_trajectories_device(nom, N, c, seed=17, out=a)
+    ob.sample_trajectories_device(nom, N, c, seed=17, out=b)
+    assert torch.equal(a, b), int((a != b).any(-1).sum())
+    flat = a.view(O * T, N, 2)
+    for begin in (1, 1601, O * T - 2):
+        part = ob.sample_units_device(nom, N, begin, 2, c, seed=17)
+        assert torch.equal(part, flat[begin:begin + 2]), begin
+    L = np.linalg.cholesky(c)
+    want = ps.sample_trajectories(nom[:1, :3].cpu().numpy(), N, (L[0, 0], L[1, 0], L[1, 1]), 17, 0, True)
+    np.testing.assert_allclose(a[:1, :3].cpu().numpy(), want, rtol=0, atol=1e-14)
+    del a, b, flat
+
+
 def test_device_sampler_unit_range_validation():
     import torch
     if not torch.cuda.is_available():
