@@ -4,8 +4,9 @@
 # batches sharded over the ranks, every exchange form — the RCCL-style all-gather (here gloo,
 # through the host), the same pipelined by chunks, and the peer-push exchange (IPC-mapped regions,
 # the ranks sharing the one GPU) — with their rank-max phase splits; C5 also the full MPC loop);
-# 4 ranks: the metric line and both legs without the MPC loops.
-# Logs: $OUTDIR (default gpurun_out/dist)/dist_{2,4}.log.
+# 4 ranks: the metric line and both legs without the MPC loops; 8 ranks (the driver's largest N):
+# everything, main.py's three filters on ranks 0-2 and ranks 3-7 with none (RANKS="2 4 8" default).
+# Logs: $OUTDIR (default gpurun_out/dist)/dist_{2,4,8}.log.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -23,11 +24,11 @@ for w, s in (d.get('strong_scaling') or {}).items():
     if s.get('main_flow'):
         print($1, 'strong', w, 'main_flow', s['main_flow']['ms_per_step'], s['main_flow']['rank0_filters'], s['main_flow']['rank0_qp_iterations'])"
 }
-timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29502 bench.py --gpus 2 --steps 400 --warmup 50 --dist-backend gloo --no-cpu-baseline \
-  > $OUT/dist_2.log 2>&1 || { tail -30 $OUT/dist_2.log; exit 2; }
-show 2 $OUT/dist_2.log
-timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
-  --master-port 29504 bench.py --gpus 4 --steps 400 --warmup 50 --dist-backend gloo --no-mpc \
-  --no-cpu-baseline > $OUT/dist_4.log 2>&1 || { tail -30 $OUT/dist_4.log; exit 3; }
-show 4 $OUT/dist_4.log
+for n in ${RANKS:-2 4 8}; do
+  extra=""
+  [ "$n" = 4 ] && extra="--no-mpc"
+  timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+    --master-port $((29500 + n)) bench.py --gpus $n --steps 400 --warmup 50 --dist-backend gloo $extra \
+    --no-cpu-baseline > $OUT/dist_$n.log 2>&1 || { tail -30 $OUT/dist_$n.log; exit $n; }
+  show $n $OUT/dist_$n.log
+done
