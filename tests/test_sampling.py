@@ -291,6 +291,23 @@ def test_device_sampler_full_blocks_repeatable_and_mirrored(dev, cov):
     del a, b, flat
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cov", [np.diag([1e-6, 1e-6]), np.diag([9.0, 9.0]), np.diag([0.01, 0.04]),
+                                 np.array([[0.04, 0.01], [0.01, 0.04]])])
+def test_device_sampler_covariance_forms_match_mirror(dev, cov):
+    """Each covariance form against the mirror, on full-block and checked workgroups (N = 4097:
+    2 049 pairs, the first workgroup's 2 048 full): isotropic at a small and a large scale (the scale
+    carried by the log's coefficients and table), diagonal but not isotropic and a correlated one
+    with equal variances (both nominal + L z)."""
+    from oracle import philox_sampler as ps
+    O, T, N = 2, 3, 4097
+    nom = _nominal(dev, O, T)
+    got = ob.sample_trajectories_device(nom, N, cov, seed=5, stream_offset=2).cpu().numpy()
+    L = np.linalg.cholesky(cov)
+    want = ps.sample_trajectories(nom.cpu().numpy(), N, (L[0, 0], L[1, 0], L[1, 1]), 5, 2, True)
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-14 * max(1.0, float(L[0, 0])))
+
+
 def test_device_sampler_unit_range_validation():
     import torch
     if not torch.cuda.is_available():
