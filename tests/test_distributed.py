@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: the multi-GPU partition + all-gather path
+"""CPU, world sizes 2, 4 and 8 over gloo: the multi-GPU partition + all-gather path
 (sharding.sharded_safe_halfspaces) reassembles exactly the single-process result.  The per-shard
 compute is the C oracle here (test-only injection); on the GPU box it is the HIP engine."""
 import os
@@ -85,7 +85,7 @@ def test_block_alignment():
     assert sharding.shard_bounds(3, 2, 1, align=4) == (3, 3)
 
 
-# ---- ShardedBatch (the form bench.py times) at world sizes 2 and 4, chunked and not -------------
+# ---- ShardedBatch (the form bench.py times) at world sizes 2, 4 and 8, chunked and not ---------
 
 def _global_batch(O, T, N):
     rng = np.random.default_rng(7)
@@ -129,10 +129,12 @@ def _sharded_worker(rank, world, port, O, T, N, chunk_list, q):
     (2, 3, 5, 40, [1, 2]), (4, 3, 5, 40, [1, 2, 4]),
     (4, 1, 5, 17, [1, 2, 3]),      # U = 5 over 4 ranks: the tail rank(s) hold zero units
     (4, 6, 7, 30, [1, 2]), (2, 1, 1, 9, [1, 2]),
+    (8, 4, 6, 30, [1, 2]),         # the driver's largest N: 3 units per rank
+    (8, 1, 5, 17, [1, 2]),         # U = 5 over 8 ranks: three ranks with zero units
 ])
 def test_sharded_batch_steps_match_single_process(world, O, T, N, chunk_list):
     """bench.py's strong-scaling step (sharding.ShardedBatch: per-rank draw, the kernel into the
-    all-gather input, the exchange — pipelined by chunks or not) at world sizes 2 and 4 over gloo,
+    all-gather input, the exchange — pipelined by chunks or not) at world sizes 2, 4 and 8 over gloo,
     with the C oracle as the shard compute: every rank ends with exactly the single-process
     records, every chunking gives the same bytes, blocks tile [0, U), and a rank with no units
     takes part in every collective; the graph-vs-eager vote is unanimous."""
