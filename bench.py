@@ -30,6 +30,8 @@ Prints ONE JSON line on rank 0: value = units of all ranks / max rank time, plus
                   (N=1: HIP events over the timed region / K, launch gaps included)
   strong_scaling  {c4, c5}: global batch sharded over N ranks (+ all-gather), phase splits
   roofline_large  (N=1) the kernel on the resident 2 GB C5 batch, graph-replayed, event-timed
+  roofline_c3_replicated  (N=1) the C3 launch plan over C3 replicated to a 2 GB working set
+                  (BASELINE.md §3's roofline convention for the cache-resident configs)
   cpu_baseline    oracle/drcvar_oracle.c (1 thread) on whole batches of the same workload
   max_abs_err     max |offset - oracle| over the benchmarked batch (the metric's second half)
 """
