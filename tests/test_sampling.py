@@ -292,15 +292,17 @@ def test_device_sampler_full_blocks_repeatable_and_mirrored(dev, cov):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cov", [np.diag([1e-6, 1e-6]), np.diag([9.0, 9.0]), np.diag([0.01, 0.04]),
-                                 np.array([[0.04, 0.01], [0.01, 0.04]])])
-def test_device_sampler_covariance_forms_match_mirror(dev, cov):
+@pytest.mark.parametrize("cov,N", [(np.diag([1e-6, 1e-6]), 4097), (np.diag([9.0, 9.0]), 4097),
+                                   (np.diag([0.01, 0.04]), 4097),
+                                   (np.array([[0.04, 0.01], [0.01, 0.04]]), 4097),
+                                   (np.diag([0.01, 0.01]), 4096), (np.diag([0.01, 0.04]), 4096)])
+def test_device_sampler_covariance_forms_match_mirror(dev, cov, N):
     """Each covariance form against the mirror, on full-block and checked workgroups (N = 4097:
-    2 049 pairs, the first workgroup's 2 048 full): isotropic at a small and a large scale (the scale
-    carried by the log's coefficients and table), diagonal but not isotropic and a correlated one
-    with equal variances (both nominal + L z)."""
+    2 049 pairs, the first workgroup's 2 048 full; N = 4096: exactly one full workgroup per unit):
+    isotropic at a small and a large scale (the scale carried by the log's coefficients and table),
+    diagonal but not isotropic and a correlated one with equal variances (both nominal + L z)."""
     from oracle import philox_sampler as ps
-    O, T, N = 2, 3, 4097
+    O, T = 2, 3
     nom = _nominal(dev, O, T)
     got = ob.sample_trajectories_device(nom, N, cov, seed=5, stream_offset=2).cpu().numpy()
     L = np.linalg.cholesky(cov)
