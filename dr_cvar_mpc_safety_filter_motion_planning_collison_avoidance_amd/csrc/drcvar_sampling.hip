@@ -30,6 +30,10 @@
 // literals in drcvar_sampling_tables.inc); the host mirror oracle/philox_sampler.py reads the same
 // file.  Accuracy: log within a few ulp, cos / sin within ~2e-16 of extended-precision references
 // (tests/test_sampling.py); kernel vs mirror to 1e-14 (FMA contraction only).
+// Round 6 (78 -> 67 VALU per sample in the loop): an isotropic covariance l^2 I rides
+// in the log (LogScale: the sample is nominal + sqrt(l^2 (-2 log u)) (cos, sin), two fmas); Philox's
+// uniform round words are made on the host (PhiloxUniform); workgroups whose pair range lies wholly
+// in the unit store with no per-pair test (store_at).
 
 #include <hip/hip_runtime.h>
 
