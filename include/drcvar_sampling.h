@@ -16,7 +16,9 @@
  *
  * Random numbers: Philox4x32-10 (counter-based; key = seed, counter = (unit * ceil(N/2) + pair,
  * stream)), one call per PAIR of samples of a unit -> two (32-bit uniform, 32-bit turn) pairs ->
- * Box-Muller -> z ~ N(0, I2); sample = nominal + L z with L the lower Cholesky factor of noise_cov.
+ * Box-Muller -> z ~ N(0, I2); sample = nominal + L z with L the lower Cholesky factor of noise_cov
+ * (for L = l I, l > 0 — the reference's default — the kernel folds l^2 into the log of Box-Muller
+ * and adds l z directly: the same values to a few ulp).
  * Tail: the radius uniform is 32-bit (u = (2x + 1) 2^-33 >= 2^-33), so |z| <= sqrt(66 ln 2) = 6.76
  * and the far tail is quantised in steps of 2^-32 in u; the reference's 53-bit draws exceed 6.76 sd
  * with probability 2^-33 per sample (~0.0075 samples per 128 M-sample C5 refill).  Below the cap the
