@@ -269,7 +269,10 @@ class Stepper:
 
     def describe(self):
         backend = dist.get_backend() if dist.is_initialized() else None
-        if getattr(self.sb, "peer", None) is not None:
+        if getattr(self.sb, "peer", None) is not None and self.sb.peer.mode == "pull":
+            coll = ("peer-pull exchange (records written into the own region by the kernel; "
+                    "publish/wait/copy-from-every-region launch)")
+        elif getattr(self.sb, "peer", None) is not None:
             coll = "peer-push exchange (records written into every rank's region by the kernel; publish/wait/copy launch)"
         else:
             coll = f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend})"
@@ -337,9 +340,10 @@ def main():
     ap.add_argument("--chunks", default="auto",
                     help="strong-scaling legs at N > 1: also time the RCCL step pipelined in these chunk "
                          "counts (comma-separated; auto = per workload, CHUNKS)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "peer"],
-                    help="strong-scaling legs at N > 1: auto = time the RCCL all-gather and the peer-push "
-                         "exchange and report the faster as the leg's step; rccl / peer = that one only")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "peer", "peer_pull"],
+                    help="strong-scaling legs at N > 1: auto = time the RCCL all-gather and the two peer "
+                         "exchanges (push, pull) and report the fastest as the leg's step; "
+                         "rccl / peer / peer_pull = that one only")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -517,7 +521,7 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload,
     exchanges = {"rccl": {"ms_per_step": elapsed / K * 1e3, "launch": launch,
                           "what": "all_gather_into_tensor of the 64-B records after the kernel"}}
     best, best_el, best_sb = "rccl", elapsed, sb
-    peer_ms = None
+    peer_ms = pull_ms = None
     if world > 1:
         ref = sb.records()
         chunk_list = CHUNKS[workload] if args.chunks == "auto" else [int(c) for c in args.chunks.split(",") if c]
@@ -539,40 +543,51 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload,
                     best, best_el, best_sb = f"rccl_chunks{c}", el_c, sbc
                 else:
                     del sbc
-        if args.exchange in ("auto", "peer"):   # (gloo rehearsal too: ranks sharing one GPU map each other)
+        # the peer forms (gloo rehearsal too: ranks sharing one GPU map each other): push — the
+        # kernel writes every record into every rank's region; pull — into its own region only,
+        # the small launch reads every rank's rows from that rank's region
+        what = {"peer": "the kernel writes every record into every rank's region (IPC-mapped, xGMI); "
+                        "one launch publishes the step, waits for every peer's and copies",
+                "peer_pull": "the kernel writes its records into its own region; one launch publishes "
+                             "the step, waits for every peer's and copies every rank's rows from that "
+                             "rank's region (IPC-mapped, xGMI)"}
+        for form in ("peer", "peer_pull"):
+            if args.exchange not in ("auto", form):
+                continue
             try:
                 sbp = sharding.ShardedBatch(nominal, ego, N, params, world, rank, seed=seed,
-                                            exchange="peer", ctrl=ctrl, samples=sb.samples,
+                                            exchange=form, ctrl=ctrl, samples=sb.samples,
                                             peer_spin_us=PEER_SPIN_US)
             except sharding.PeerExchangeUnavailable as exc:
-                exchanges["peer"] = {"unavailable": str(exc)}
-                sbp = None
-            if sbp is not None:
-                el_p, launch_p = run_form(sbp, lambda: (None if sbp.peer.error() == 0 else
-                                                        f"a wait gave up (error word {sbp.peer.error():#x})"))
-            if sbp is not None and el_p is None:
-                exchanges["peer"] = {"unavailable": launch_p}
+                exchanges[form] = {"unavailable": str(exc)}
+                continue
+            el_p, launch_p = run_form(sbp, lambda: (None if sbp.peer.error() == 0 else
+                                                    f"a wait gave up (error word {sbp.peer.error():#x})"))
+            if el_p is None:
+                exchanges[form] = {"unavailable": launch_p}
                 sbp.close()
-                sbp = None
-            if sbp is not None:
-                err = sbp.peer.error()
-                same = err == 0 and bool(torch.equal(sbp.records().to(ref.device), ref))
-                same = agree(world, ctrl, same)
-                pst = Stepper(sbp, mode, 10, K, dev, compute=False, world=world, ctrl=ctrl)
-                pst.run(min(K, 10))
-                _, peer_s, _ = timed(world, lambda: pst.run(K), dev, stream)
-                del pst
+                continue
+            err = sbp.peer.error()
+            same = err == 0 and bool(torch.equal(sbp.records().to(ref.device), ref))
+            same = agree(world, ctrl, same)
+            pst = Stepper(sbp, mode, 10, K, dev, compute=False, world=world, ctrl=ctrl)
+            pst.run(min(K, 10))
+            _, peer_s, _ = timed(world, lambda: pst.run(K), dev, stream)
+            del pst
+            if form == "peer":
                 peer_ms = peer_s / K * 1e3
-                exchanges["peer"] = {
-                    "ms_per_step": el_p / K * 1e3, "records_equal_rccl": same, "error_word": err,
-                    "launch": launch_p, "exchange_alone_ms": peer_ms,
-                    "what": "the kernel writes every record into every rank's region (IPC-mapped, "
-                            "xGMI); one launch publishes the step, waits for every peer's and copies"}
-                if same and el_p < best_el:
-                    best, best_el, best_sb = "peer", el_p, sbp
-                else:
-                    sbp.close()
-                    del sbp
+            else:
+                pull_ms = peer_s / K * 1e3
+            exchanges[form] = {
+                "ms_per_step": el_p / K * 1e3, "records_equal_rccl": same, "error_word": err,
+                "launch": launch_p, "exchange_alone_ms": peer_s / K * 1e3, "what": what[form]}
+            if same and el_p < best_el:   # (el_p, best_el: rank maxima; same: agreed)
+                if best in what:
+                    best_sb.close()       # collective, on every rank alike
+                best, best_el, best_sb = form, el_p, sbp
+            else:
+                sbp.close()
+                del sbp
     out = {"workload": f"{workload}: {desc}, global batch sharded over {world} rank(s)",
            "value": sb.U * K / best_el, "unit": "halfspace-constraints/s", "n_gpus": world,
            "steps": K, "ms_per_step": best_el / K * 1e3, "scaling": "strong",
@@ -584,7 +599,7 @@ def strong_scaling(args, world, rank, dev, stream, params, gdev, mode, workload,
                                            if world > 1 else ""),
            "launch": exchanges[best]["launch"],
            "phases_rank_max": {"kernel_ms": kernel_s * 1e3, "allgather_ms": gather_ms,
-                               "peer_exchange_ms": peer_ms,
+                               "peer_exchange_ms": peer_ms, "peer_pull_exchange_ms": pull_ms,
                                "timing": f"HIP events over {K} steps of the phase alone, max over ranks"},
            "kernel_roofline_frac": sb.algorithmic_bytes / kernel_s / HBM_PEAK,
            # one rank: HBM bytes per launch of the whole batch from the committed PMC passes

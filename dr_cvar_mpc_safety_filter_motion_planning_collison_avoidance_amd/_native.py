@@ -105,6 +105,7 @@ EXPORTED_SYMBOLS = (
     "drcvar_peer_bus_id",
     "drcvar_peer_device_of",
     "drcvar_peer_signal_wait",
+    "drcvar_peer_signal_wait_pull",
     "drcvar_safe_halfspaces_f64_peer",
 )
 
@@ -339,6 +340,8 @@ def _bind(lib):
     lib.drcvar_peer_device_of.restype = ctypes.c_int
     lib.drcvar_peer_signal_wait.argtypes = [peerp, ptr, i64, ptr]
     lib.drcvar_peer_signal_wait.restype = ctypes.c_int
+    lib.drcvar_peer_signal_wait_pull.argtypes = [peerp, ptr, i64, ptr]
+    lib.drcvar_peer_signal_wait_pull.restype = ctypes.c_int
     lib.drcvar_safe_halfspaces_f64_peer.argtypes = [
         ptr, i64, i64, i64, i64, i64, i64, ptr, i64, dbl, dbl, dbl, dbl, dbl, peerp, i64, ptr, ptr]
     lib.drcvar_safe_halfspaces_f64_peer.restype = ctypes.c_int

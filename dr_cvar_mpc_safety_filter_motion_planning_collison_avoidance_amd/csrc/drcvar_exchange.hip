@@ -22,6 +22,15 @@
 //
 // The grid is at most 256 workgroups of 256 threads (one per 4 K records); no workgroup waits on
 // another of the launch (each polls the flags itself), so residency does not matter.
+//
+// The pull form (drcvar_peer_signal_wait_pull): the halfspace launch wrote its records into its
+// own region only (drcvar_safe_halfspaces_f64_peer with the one-rank set {own region}: its waves
+// wait for local acknowledgements, not for a write round trip over xGMI per unit); this launch
+// publishes the same way, waits the same way, and copies rank j's rows of the parity buffer from
+// rank j's region (nontemporal 16-B loads over xGMI).  Double buffering holds as in the push form:
+// a rank rewrites parity p two steps later, after every peer has published the step in between,
+// which each does only after its copy of parity p has completed (the previous launch on its
+// stream).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,6 +50,27 @@ __device__ __forceinline__ unsigned long long* flags_of(double* region, int64_t 
   return reinterpret_cast<unsigned long long*>(region + 2 * rows * DRCVAR_OUT_WIDTH);
 }
 
+// n2 16-B elements src -> dst by the whole grid, kPerThread loads in flight per thread per pass
+// (the uncached region answers from HBM: one round trip per pass, not per element)
+__device__ __forceinline__ void copy_block(const dbl2* __restrict__ src, dbl2* __restrict__ dst, int64_t n2) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i0 < n2;
+       i0 += stride * kPerThread) {
+    dbl2 v[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int64_t i = i0 + k * stride;
+      if (i < n2) v[k] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int64_t i = i0 + k * stride;
+      if (i < n2) dst[i] = v[k];
+    }
+  }
+}
+
+template <bool kPull>
 __global__ void __launch_bounds__(kThreads)
 peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long spin_ticks) {
   const int tid = threadIdx.x;
@@ -49,7 +79,7 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
   // launch advances it only after every workgroup has read it)
   const unsigned long long g = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
   const int64_t parity = static_cast<int64_t>(g & 1ull);
-  if (blockIdx.x == 0 && tid < ps.n_ranks) {  // publish: this rank's rows are in every region
+  if (blockIdx.x == 0 && tid < ps.n_ranks) {  // publish: this rank's rows are in every region (pull: in its own)
     __hip_atomic_store(flags_of(ps.region[tid], ps.rows) + ps.rank, g, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -66,24 +96,16 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
     }
   }
   __syncthreads();
-  // copy: the gathered parity buffer -> out, kPerThread 16-B loads in flight per thread per pass
-  // (the uncached region answers from HBM: one round trip per pass, not per element)
-  const dbl2* src = reinterpret_cast<const dbl2*>(ps.region[ps.rank] + parity * ps.rows * DRCVAR_OUT_WIDTH);
+  // copy: the gathered parity buffer -> out (pull: rank j's rows from rank j's region)
   dbl2* dst = reinterpret_cast<dbl2*>(out);
-  const int64_t n2 = ps.rows * DRCVAR_OUT_WIDTH / 2;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kThreads + tid; i0 < n2; i0 += stride * kPerThread) {
-    dbl2 v[kPerThread];
-#pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {
-      const int64_t i = i0 + k * stride;
-      if (i < n2) v[k] = __builtin_nontemporal_load(src + i);
-    }
-#pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {
-      const int64_t i = i0 + k * stride;
-      if (i < n2) dst[i] = v[k];
-    }
+  if constexpr (!kPull) {
+    copy_block(reinterpret_cast<const dbl2*>(ps.region[ps.rank] + parity * ps.rows * DRCVAR_OUT_WIDTH),
+               dst, ps.rows * DRCVAR_OUT_WIDTH / 2);
+  } else {
+    const int64_t per = ps.rows / ps.n_ranks;  // (host-checked: rows = n_ranks * per)
+    for (int j = 0; j < ps.n_ranks; ++j)
+      copy_block(reinterpret_cast<const dbl2*>(ps.region[j] + (parity * ps.rows + j * per) * DRCVAR_OUT_WIDTH),
+                 dst + j * per * (DRCVAR_OUT_WIDTH / 2), per * DRCVAR_OUT_WIDTH / 2);
   }
   // advance: the last workgroup out stores the generation
   __syncthreads();
@@ -104,6 +126,20 @@ bool valid(const drcvar_peer_set* ps) {
   for (int j = 0; j < ps->n_ranks; ++j)
     if (!ps->region[j]) return false;
   return true;
+}
+
+template <bool kPull>
+int signal_wait(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us, void* stream) {
+  if (!valid(peers) || !out || spin_limit_us <= 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  if (kPull && peers->rows % peers->n_ranks != 0) return DRCVAR_ERR_INVALID_ARGUMENT;
+  const int64_t n2 = peers->rows * DRCVAR_OUT_WIDTH / 2;
+  int64_t groups = (n2 + kThreads * kPerThread - 1) / (kThreads * kPerThread);
+  groups = groups < 1 ? 1 : (groups > kMaxGroups ? kMaxGroups : groups);
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(peer_signal_wait_kernel<kPull>, dim3(static_cast<unsigned>(groups)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), *peers, out,
+                     static_cast<long long>(spin_limit_us) * 100);  // 100 MHz realtime clock
+  return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
 }
 
 }  // namespace
@@ -177,17 +213,15 @@ int drcvar_peer_device_of(const char* bus_id, int32_t* device) {
   return DRCVAR_OK;
 }
 
+
 int drcvar_peer_signal_wait(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us,
                             void* stream) {
-  if (!valid(peers) || !out || spin_limit_us <= 0) return DRCVAR_ERR_INVALID_ARGUMENT;
-  const int64_t n2 = peers->rows * DRCVAR_OUT_WIDTH / 2;
-  int64_t groups = (n2 + kThreads * kPerThread - 1) / (kThreads * kPerThread);
-  groups = groups < 1 ? 1 : (groups > kMaxGroups ? kMaxGroups : groups);
-  (void)hipGetLastError();
-  hipLaunchKernelGGL(peer_signal_wait_kernel, dim3(static_cast<unsigned>(groups)), dim3(kThreads), 0,
-                     static_cast<hipStream_t>(stream), *peers, out,
-                     static_cast<long long>(spin_limit_us) * 100);  // 100 MHz realtime clock
-  return hipGetLastError() == hipSuccess ? DRCVAR_OK : DRCVAR_ERR_LAUNCH;
+  return signal_wait<false>(peers, out, spin_limit_us, stream);
+}
+
+int drcvar_peer_signal_wait_pull(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us,
+                                 void* stream) {
+  return signal_wait<true>(peers, out, spin_limit_us, stream);
 }
 
 }  // extern "C"

@@ -32,7 +32,10 @@ Two exchanges for :class:`ShardedBatch`:
   generation and copies the gathered records out — the exchange rides inside the kernel and only
   a flag round trip is left after it.  Set up only when every rank can map every peer's memory;
   all ranks agree (over the control group) before any rank uses it, otherwise every rank keeps
-  ``"rccl"``.
+  ``"rccl"``;
+* ``"peer_pull"`` — the same regions and flags, but each rank's launch writes its records into its
+  own region only and the small launch copies every rank's rows from that rank's region (reads
+  over xGMI): no write round trip over xGMI inside the halfspace kernel's units.
 
 ``compute`` is injectable in :func:`sharded_safe_halfspaces`, and the sampler / launch preparation
 in :class:`ShardedBatch`, so the partition/gather logic can be exercised with world_size 2 and 4
@@ -67,7 +70,12 @@ class PeerExchange:
     non-zero instead of a hang)."""
 
     def __init__(self, rows: int, world: int, rank: int, device: torch.device, ctrl=None,
-                 spin_limit_us: int = 2_000_000):
+                 spin_limit_us: int = 2_000_000, mode: str = "push"):
+        if mode not in ("push", "pull"):
+            raise ValueError(f"mode must be 'push' or 'pull', not {mode!r}")
+        if mode == "pull" and rows % world:
+            raise ValueError(f"the pull form needs rows ({rows}) = world ({world}) * rows per rank")
+        self.mode = mode
         if not (1 <= world <= _native.MAX_PEERS):
             raise PeerExchangeUnavailable(f"peer exchange supports 1..{_native.MAX_PEERS} ranks, not {world}")
         lib = _native.lib()
@@ -134,6 +142,13 @@ class PeerExchange:
         ps.rows, ps.state, ps.n_ranks, ps.rank = self.rows, self.state.data_ptr(), world, rank
         self.peers = ps
         self._ps_ref = ctypes.pointer(ps)
+        # the pull form's halfspace launches write into the own region only: a one-rank set
+        local = _native.PeerSet()
+        local.region[0] = regions[rank]
+        local.rows, local.state, local.n_ranks, local.rank = self.rows, self.state.data_ptr(), 1, 0
+        self._local = local
+        self._launch_ref = ctypes.pointer(local) if mode == "pull" else self._ps_ref
+        self._signal = lib.drcvar_peer_signal_wait_pull if mode == "pull" else lib.drcvar_peer_signal_wait
         self._out_ptr = ctypes.c_void_p(self.out.data_ptr())
         self._spin = ctypes.c_int64(self.spin_limit_us)
 
@@ -141,8 +156,7 @@ class PeerExchange:
         """Publish this rank's step, wait for every peer's, copy the gathered records to ``out``
         (one launch on ``stream``, default the current stream)."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        code = self._lib.drcvar_peer_signal_wait(self._ps_ref, self._out_ptr, self._spin,
-                                                  ctypes.c_void_p(int(s.cuda_stream)))
+        code = self._signal(self._ps_ref, self._out_ptr, self._spin, ctypes.c_void_p(int(s.cuda_stream)))
         if code != _native.OK:
             _native.check(code)
 
@@ -159,7 +173,7 @@ class PeerExchange:
         args = (ctypes.c_void_p(samples.data_ptr()), O, T, N, samples.stride(0), samples.stride(1),
                 samples.stride(2), ctypes.c_void_p(ego.data_ptr()), ego.stride(0),
                 params.robot_radius, params.obstacle_radius, params.alpha, params.delta, params.epsilon,
-                self._ps_ref, int(row_base), ctypes.c_void_p(None),
+                self._launch_ref, int(row_base), ctypes.c_void_p(None),
                 ctypes.c_void_p(engine._stream_handle(samples.device, stream)))
         return engine.PreparedLaunch(self._lib.drcvar_safe_halfspaces_f64_peer, args, (samples, ego, self))
 
@@ -362,7 +376,8 @@ class ShardedBatch:
     ``exchange="peer"``: a :class:`PeerExchange` (collective set-up over ``ctrl``; raises
     :class:`PeerExchangeUnavailable` on every rank when any rank cannot use it) — the kernel writes
     every record into every rank's region and :meth:`step` adds the one publish/wait/copy launch;
-    ``full`` is the exchange's output.  ``records()`` is the global ``[O, T, 8]`` either way.
+    ``exchange="peer_pull"``: the kernel writes into the own region only and that launch copies
+    every rank's rows from its region; ``full`` is the exchange's output.  ``records()`` is the global ``[O, T, 8]`` either way.
 
     ``sample_fn(nominal, n, start, count, cov, seed=, stream_offset=, zero_first_step=)`` and
     ``prepare_fn(samples [1, c, N, 2], ego [c, 2], params, out [1, c, 8], stream)`` are test-only
@@ -378,9 +393,9 @@ class ShardedBatch:
                  exchange: str = "rccl", ctrl=None, sample_fn=None, prepare_fn=None,
                  samples: torch.Tensor | None = None, peer_spin_us: int = 2_000_000):
         from .simulation import obstacles
-        if exchange not in ("rccl", "peer"):
-            raise ValueError(f"exchange must be 'rccl' or 'peer', not {exchange!r}")
-        if exchange == "peer" and (chunks != 1 or gather_device is not None):
+        if exchange not in ("rccl", "peer", "peer_pull"):
+            raise ValueError(f"exchange must be 'rccl', 'peer' or 'peer_pull', not {exchange!r}")
+        if exchange != "rccl" and (chunks != 1 or gather_device is not None):
             raise ValueError("the peer exchange runs inside the kernel: one chunk, device records")
         O, T = int(nominal.shape[0]), int(nominal.shape[1])
         dev = nominal.device
@@ -412,9 +427,10 @@ class ShardedBatch:
         self.exchange_kind = exchange if do_exchange else None
         self.peer = None
         self.scratch = None
-        if do_exchange and exchange == "peer":
+        if do_exchange and exchange != "rccl":
             self.peer = PeerExchange(self.per * world_size, world_size, rank, dev, ctrl=ctrl,
-                                     spin_limit_us=peer_spin_us)
+                                     spin_limit_us=peer_spin_us,
+                                     mode="pull" if exchange == "peer_pull" else "push")
             self.full = self.peer.out
         else:
             self.full = (torch.empty((self.per * world_size, engine.OUT_WIDTH), dtype=torch.float64,

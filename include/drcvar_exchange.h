@@ -72,6 +72,14 @@ int drcvar_peer_device_of(const char* bus_id, int32_t* device);
 int drcvar_peer_signal_wait(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us,
                             void* stream);
 
+/* The pull form of the step: every rank's halfspace launch wrote its rows into its OWN region only
+   (drcvar_safe_halfspaces_f64_peer with the one-rank set {region = {own}, rows, state, n_ranks 1,
+   rank 0}: no write round trip over xGMI per unit); this launch publishes and waits as
+   drcvar_peer_signal_wait does and copies rank j's rows [j per, (j + 1) per) of the step's parity
+   buffer from rank j's region.  rows must be n_ranks * per. */
+int drcvar_peer_signal_wait_pull(const drcvar_peer_set* peers, double* out, int64_t spin_limit_us,
+                                 void* stream);
+
 /*
  * drcvar_safe_halfspaces_f64_v2 (include/drcvar_halfspace.h) in the peer-push form: unit u of the
  * launch (u = o * n_steps + t) is written to global row row_base + u of every rank's region in the

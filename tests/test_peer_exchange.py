@@ -1,4 +1,6 @@
-"""GPU: the peer-push record exchange (include/drcvar_exchange.h, sharding.PeerExchange).
+"""GPU: the peer record exchange (include/drcvar_exchange.h, sharding.PeerExchange), in both forms:
+push (the kernel writes every record into every rank's region) and pull (into its own region; the
+small launch copies every rank's rows from that rank's region).
 
 * one rank (the exchange with itself): ShardedBatch(exchange="peer") gives bitwise the records of
   the plain launch, step after step, eager and replayed from a hipGraph, the generation counts the
@@ -47,10 +49,11 @@ def _whole(O, T, N, dev, seed):
     return nominal, ego, engine.safe_halfspaces(s, ego, RiskParams())
 
 
+@pytest.mark.parametrize("form", ["peer", "peer_pull"])
 @pytest.mark.parametrize("O,T,N", [(10, 20, 1000), (7, 9, 300), (3, 5, 5000)])
-def test_peer_exchange_one_rank_matches_plain_launch(dev, O, T, N):
+def test_peer_exchange_one_rank_matches_plain_launch(dev, O, T, N, form):
     nominal, ego, whole = _whole(O, T, N, dev, seed=5)
-    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, seed=5, exchange="peer",
+    sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), 1, 0, seed=5, exchange=form,
                                force_exchange=True)
     assert sb.peer is not None and sb.peer.rows == O * T
     for k in range(3):                                  # both parities, then the first again
@@ -73,7 +76,7 @@ def test_peer_exchange_one_rank_matches_plain_launch(dev, O, T, N):
     sb.close()
 
 
-def _two_rank_worker(rank, world, port, O, T, N, q):
+def _two_rank_worker(rank, world, port, O, T, N, q, form="peer"):
     import sys
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -82,7 +85,7 @@ def _two_rank_worker(rank, world, port, O, T, N, q):
     torch.cuda.set_device(dev)
     try:
         nominal, ego, whole = _whole(O, T, N, dev, seed=9)
-        sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), world, rank, seed=9, exchange="peer")
+        sb = sharding.ShardedBatch(nominal, ego, N, RiskParams(), world, rank, seed=9, exchange=form)
         ok = []
         for k in range(3):
             sb.step()
@@ -102,7 +105,8 @@ def _two_rank_worker(rank, world, port, O, T, N, q):
         gen, err = sb.peer.generation(), sb.peer.error()
         sb.close()
         # the failure path: rank 1 never signals, rank 0's wait gives up at its spin limit
-        px = sharding.PeerExchange(8, world, rank, dev, spin_limit_us=50_000)
+        px = sharding.PeerExchange(8, world, rank, dev, spin_limit_us=50_000,
+                                   mode="pull" if form == "peer_pull" else "push")
         if rank == 0:
             px.signal_wait()
             torch.cuda.synchronize(dev)
@@ -115,12 +119,13 @@ def _two_rank_worker(rank, world, port, O, T, N, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("form", ["peer", "peer_pull"])
 @pytest.mark.parametrize("O,T,N", [(10, 20, 1000), (5, 3, 64)])
-def test_peer_exchange_two_processes_one_gpu(dev, O, T, N):
+def test_peer_exchange_two_processes_one_gpu(dev, O, T, N, form):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, O, T, N, q)) for r in range(2)]
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, O, T, N, q, form)) for r in range(2)]
     for p in procs:
         p.start()
     results = sorted(q.get(timeout=240) for _ in procs)
