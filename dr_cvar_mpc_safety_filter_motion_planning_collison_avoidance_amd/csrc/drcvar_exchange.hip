@@ -102,10 +102,28 @@ peer_signal_wait_kernel(drcvar_peer_set ps, double* __restrict__ out, long long 
     copy_block(reinterpret_cast<const dbl2*>(ps.region[ps.rank] + parity * ps.rows * DRCVAR_OUT_WIDTH),
                dst, ps.rows * DRCVAR_OUT_WIDTH / 2);
   } else {
-    const int64_t per = ps.rows / ps.n_ranks;  // (host-checked: rows = n_ranks * per)
-    for (int j = 0; j < ps.n_ranks; ++j)
-      copy_block(reinterpret_cast<const dbl2*>(ps.region[j] + (parity * ps.rows + j * per) * DRCVAR_OUT_WIDTH),
-                 dst + j * per * (DRCVAR_OUT_WIDTH / 2), per * DRCVAR_OUT_WIDTH / 2);
+    // every rank's block in ONE pass, the loads of a thread (from any peers) issued together: a
+    // pass per peer would put one xGMI round trip per peer in series
+    const int64_t per2 = ps.rows / ps.n_ranks * (DRCVAR_OUT_WIDTH / 2);  // (host-checked: rows = n_ranks * per)
+    const int64_t n2 = ps.rows * (DRCVAR_OUT_WIDTH / 2), base = parity * n2;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+    for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kThreads + tid; i0 < n2; i0 += stride * kPerThread) {
+      dbl2 v[kPerThread];
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        const int64_t i = i0 + k * stride;
+        if (i < n2) {
+          int j = 0;
+          while (j + 1 < ps.n_ranks && i >= (j + 1) * per2) ++j;  // the rank whose block holds i
+          v[k] = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(ps.region[j]) + base + i);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        const int64_t i = i0 + k * stride;
+        if (i < n2) dst[i] = v[k];
+      }
+    }
   }
   // advance: the last workgroup out stores the generation
   __syncthreads();
