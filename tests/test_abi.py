@@ -134,6 +134,23 @@ def test_peer_exchange_host_side():
     assert peer(O=0) == _native.OK                                     # empty: nothing launched
     assert lib.drcvar_peer_alloc(0, ctypes.byref(ctypes.c_void_p()), out) == _native.ERR_INVALID_ARGUMENT
     assert lib.drcvar_peer_open(None, ctypes.byref(ctypes.c_void_p())) == _native.ERR_INVALID_ARGUMENT
+    # the pull form's own checks: every rank's block the same size (rows = n_ranks * per)
+    ps.rows = 11
+    assert lib.drcvar_peer_signal_wait_pull(ctypes.byref(ps), out, 1000, None) == _native.ERR_INVALID_ARGUMENT
+    ps.rows = 10
+    assert lib.drcvar_peer_signal_wait_pull(ctypes.byref(ps), None, 1000, None) == _native.ERR_INVALID_ARGUMENT
+    assert lib.drcvar_peer_signal_wait_pull(None, out, 1000, None) == _native.ERR_INVALID_ARGUMENT
+
+
+def test_peer_exchange_mode_checks():
+    """sharding.PeerExchange rejects an unknown form, and the pull form's uneven blocks, before it
+    touches a device."""
+    import torch
+    from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd import sharding
+    with pytest.raises(ValueError):
+        sharding.PeerExchange(8, 2, 0, torch.device("cpu"), mode="gather")
+    with pytest.raises(ValueError):
+        sharding.PeerExchange(7, 2, 0, torch.device("cpu"), mode="pull")
 
 
 def test_prepared_peer_launch_takes_the_struct_pointer():
