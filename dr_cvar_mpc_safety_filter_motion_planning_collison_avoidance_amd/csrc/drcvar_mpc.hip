@@ -167,8 +167,12 @@ constexpr double kPolishMerit = 1e-5; // polish only from an iterate this close 
 // 0.341 ms (mean 5.3 -> 3.3 iterations); every problem optimal and polished, |u - oracle| <= 7e-10.
 // From 3e-2 the guess failed on the mean filter (three attempts, then the resume: 1.02 ms); with
 // two attempts from 1e-2 one problem of the 1 024 needed the resume (0.420 ms); 1e-3 / 3e-3 /
-// 1e-4 polish one or two iterations later.
+// 1e-4 polish one or two iterations later.  With many halfspace rows (kManyRowsObstacles) the
+// threshold is 1.5e-2 (profiles/r06/early_polish/r6_final_thresholds/): the C5 fixture 8 -> 7
+// iterations, 0.479 -> 0.443 ms; main.py's mean filter and the synthetic C5 problems unchanged.
+// Few rows keep 1e-2: from 1.5e-2 the 1 024-problem batch slows 0.342 -> 0.384 ms.
 constexpr double kEarlyPolishMerit = 1e-2;
+constexpr double kEarlyPolishMeritMany = 1.5e-2;
 constexpr int kEarlyPolishAttempts = 3;  // active-set corrections of an early polish
 constexpr double kPolishDualTol = 1e-7;
 constexpr int kManyRowsObstacles = 64;  // interior-point start for many halfspace rows (below)
@@ -2376,7 +2380,7 @@ __global__ __launch_bounds__(BLK, (CL && BLK <= 256) ? 1 : 2) void mpc_ipm_kerne
         best_merit = merit;
         break;
       }
-      if (round == 0 && a.polish && merit <= kEarlyPolishMerit) {
+      if (round == 0 && a.polish && merit <= (many_rows ? kEarlyPolishMeritMany : kEarlyPolishMerit)) {
         converged = true;  // (the factorisation beside this P1 serves the active-set guess)
         early = true;
         // the best iterate is this one (u, merit and iteration together): the post-loop restore
