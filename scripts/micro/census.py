@@ -13,8 +13,11 @@ from dr_cvar_mpc_safety_filter_motion_planning_collison_avoidance_amd.core impor
 from test_mpc import _random_problem  # noqa: E402
 
 dev = torch.device("cuda", 0)
-for dyn, H, O in [("double", 30, 3), ("double", 32, 6), ("double", 40, 4), ("single", 20, 5),
-                  ("generic1", 32, 4), ("generic3", 24, 3), ("generic4", 30, 4), ("generic8", 16, 3)]:
+SHAPES = [("double", 30, 3), ("double", 32, 6), ("double", 40, 4), ("single", 20, 5),
+          ("generic1", 32, 4), ("generic3", 24, 3), ("generic4", 30, 4), ("generic8", 16, 3)]
+if os.environ.get("CENSUS_MANY"):  # problems with >= 64 obstacles (the many-rows start and polish threshold)
+    SHAPES = [("double", 30, 64), ("double", 40, 96), ("double", 20, 128), ("single", 30, 64)]
+for dyn, H, O in SHAPES:
     rng = np.random.default_rng(H * 100 + O)
     Bn = 150
     base = _random_problem(rng, O, H, H, dyn)
